@@ -1,0 +1,81 @@
+"""Golden-vector case table shared by the oracle tests and the GPU parity tests.
+
+Each case names: the arch, the synthetic input spec, and the sampler settings
+that tests/golden/make_golden.py ran the reference with. Fixtures are float32 .npz.
+"""
+
+from __future__ import annotations
+
+import os
+
+import numpy as np
+
+from f5_tts_amd import configs
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+B1 = dict(B=1, ref_frames=60, total_frames=150, n_text=30, vocab=64)
+B3 = dict(B=3, ref_frames=[40, 60, 25], total_frames=[90, 150, 70], n_text=[20, 30, 12], vocab=64)
+C1 = dict(B=1, ref_frames=282, total_frames=564, n_text=90)
+C2 = dict(B=1, ref_frames=938, total_frames=1876, n_text=300)
+
+
+def arch_of(tag):
+    if tag == "tiny":
+        return configs.get_arch("DiT_tiny", text_num_embeds=64)
+    if tag == "tiny_v0":
+        return configs.get_arch("DiT_tiny", text_num_embeds=64, text_mask_padding=False, pe_attn_head=1)
+    if tag == "tiny_masked":
+        return configs.get_arch("DiT_tiny", text_num_embeds=64, attn_mask_enabled=True)
+    if tag == "utiny":
+        return configs.get_arch("UNetT_tiny", text_num_embeds=64)
+    if tag == "c1":
+        return configs.get_arch("F5TTS_v1_Small_4L")
+    if tag == "c2":
+        return configs.get_arch("F5TTS_v1_Base")
+    raise KeyError(tag)
+
+
+# name -> (arch tag, input spec, nfe, sway, cfg)
+SAMPLE_CASES = {
+    "dit_tiny_sample_b1": ("tiny", B1, 4, -1.0, 2.0),
+    "dit_tiny_sample_b3": ("tiny", B3, 6, -1.0, 2.0),
+    "dit_tiny_sample_b3_masked": ("tiny_masked", B3, 6, -1.0, 2.0),
+    "dit_v0_tiny_sample_b3": ("tiny_v0", B3, 5, None, 2.0),
+    "dit_tiny_sample_b1_lin32": ("tiny", B1, 32, -1.0, 2.0),
+    "unett_tiny_sample_b1": ("utiny", B1, 4, -1.0, 2.0),
+    "unett_tiny_sample_b3": ("utiny", B3, 4, -1.0, 2.0),
+    "c1_sample_fp32": ("c1", C1, 4, -1.0, 2.0),
+    "c2_sample_fp32": ("c2", C2, 16, -1.0, 2.0),
+}
+
+FORWARD_CASES = {
+    "dit_tiny_fwd_b1": ("tiny", B1),
+    "dit_tiny_fwd_b3": ("tiny", B3),
+    "unett_tiny_fwd_b1": ("utiny", B1),
+    "unett_tiny_fwd_b3": ("utiny", B3),
+}
+
+SEED = 7
+FWD_T = 0.3
+
+
+def load(name):
+    path = os.path.join(GOLDEN, name + ".npz")
+    if not os.path.exists(path):
+        return None
+    with np.load(path) as z:
+        return {k: z[k] for k in z.files}
+
+
+def rel_err(a, b):
+    a = np.asarray(a, dtype=np.float64)
+    b = np.asarray(b, dtype=np.float64)
+    return float(np.linalg.norm(a - b) / max(np.linalg.norm(b), 1e-30))
+
+
+def max_rel(a, b):
+    """max |a-b| / max |b|  (the '≤1e-3 rel' figure used throughout)."""
+    a = np.asarray(a, dtype=np.float64)
+    b = np.asarray(b, dtype=np.float64)
+    return float(np.abs(a - b).max() / max(np.abs(b).max(), 1e-30))
