@@ -1,0 +1,112 @@
+// Shared device helpers for the gfx950 CFM engine (wave64, MFMA, LDS swizzles).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+typedef __bf16 bf16;
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+#define F5H_DEV __device__ __forceinline__
+#define LDS_PTR(T) __attribute__((address_space(3))) T*
+
+// ---------------------------------------------------------------- conversions
+F5H_DEV bf16 f2bf(float x) { return (bf16)x; }  // RNE, NaN-preserving (v_cvt_pk_bf16_f32)
+F5H_DEV float bf2f(bf16 x) { return (float)x; }
+
+template <typename T> F5H_DEV T from_f32(float x);
+template <> F5H_DEV float from_f32<float>(float x) { return x; }
+template <> F5H_DEV bf16 from_f32<bf16>(float x) { return f2bf(x); }
+F5H_DEV float to_f32(float x) { return x; }
+F5H_DEV float to_f32(bf16 x) { return bf2f(x); }
+
+// ---------------------------------------------------------------- activations
+F5H_DEV float gelu_tanh(float x) {  // nn.GELU(approximate="tanh"), modules.py:358
+  const float k0 = 0.7978845608028654f, k1 = 0.044715f;
+  float u = k0 * (x + k1 * x * x * x);
+  return 0.5f * x * (1.f + tanhf(u));
+}
+F5H_DEV float gelu_erf(float x) {  // nn.GELU(), modules.py:266
+  return 0.5f * x * (1.f + erff(x * 0.7071067811865476f));
+}
+F5H_DEV float softplus(float x) {  // torch softplus (threshold 20)
+  return x > 20.f ? x : log1pf(expf(x));
+}
+F5H_DEV float mish(float x) { return x * tanhf(softplus(x)); }  // nn.Mish, modules.py:181
+F5H_DEV float silu(float x) { return x / (1.f + expf(-x)); }
+
+// ---------------------------------------------------------------- wave reductions (64 lanes)
+F5H_DEV float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+F5H_DEV float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// ---------------------------------------------------------------- LDS swizzle
+// Tiles are stored as rows of 128 bytes = 8 chunks of 16 B. Chunk c of row r lives at
+// c ^ g(r), g(r) = ((r>>1)&1)<<2 | ((r>>2)&3): conflict-free for ds_read_b128 where the
+// 16 lanes of a group read 16 distinct rows at one chunk (GEMM / QK^T operands), and for
+// ds_read_b64_tr_b16 reading 4 consecutive rows x 64 B (the PV operand).
+F5H_DEV int swz128(int row, int chunk) {
+  return chunk ^ ((((row >> 1) & 1) << 2) | ((row >> 2) & 3));
+}
+// 256-byte rows (fp32 conv windows): chunk c (0..15) of row r at c ^ (r & 15).
+F5H_DEV int swz256(int row, int chunk) { return chunk ^ (row & 15); }
+
+// ---------------------------------------------------------------- MFMA per 64-byte k-slab
+// One "k-slab" is 64 bytes of K per row: 32 bf16 or 16 fp32. Each lane holds 16 bytes
+// of A (row lane&15, chunk lane>>4) and of B (col lane&15, chunk lane>>4).
+// bf16: one v_mfma_f32_16x16x32_bf16 (lane group g supplies k = 8g..8g+7).
+// fp32: four v_mfma_f32_16x16x4_f32, the j-th taking element j, so lane group g supplies
+//       k = 4g + j: every k in 0..15 is summed exactly once (permuted order).
+template <typename T> struct Slab;
+template <> struct Slab<bf16> {
+  typedef bf16x8 frag;
+  static F5H_DEV f32x4 mma(const frag& a, const frag& b, f32x4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+  }
+};
+template <> struct Slab<float> {
+  typedef f32x4 frag;
+  static F5H_DEV f32x4 mma(const frag& a, const frag& b, f32x4 c) {
+    c = __builtin_amdgcn_mfma_f32_16x16x4f32(a[0], b[0], c, 0, 0, 0);
+    c = __builtin_amdgcn_mfma_f32_16x16x4f32(a[1], b[1], c, 0, 0, 0);
+    c = __builtin_amdgcn_mfma_f32_16x16x4f32(a[2], b[2], c, 0, 0, 0);
+    c = __builtin_amdgcn_mfma_f32_16x16x4f32(a[3], b[3], c, 0, 0, 0);
+    return c;
+  }
+};
+
+// 16-byte global load of 16/sizeof(T) elements of type T starting at p, converting
+// from source type S (float or bf16) into compute type T; `ok` false -> zeros.
+template <typename T, typename S> struct Load16;
+template <> struct Load16<bf16, bf16> {
+  static F5H_DEV uint4 ld(const bf16* p, bool ok) {
+    return ok ? *reinterpret_cast<const uint4*>(p) : make_uint4(0, 0, 0, 0);
+  }
+};
+template <> struct Load16<float, float> {
+  static F5H_DEV uint4 ld(const float* p, bool ok) {
+    return ok ? *reinterpret_cast<const uint4*>(p) : make_uint4(0, 0, 0, 0);
+  }
+};
+template <> struct Load16<bf16, float> {
+  static F5H_DEV uint4 ld(const float* p, bool ok) {
+    if (!ok) return make_uint4(0, 0, 0, 0);
+    float4 a = *reinterpret_cast<const float4*>(p);
+    float4 b = *reinterpret_cast<const float4*>(p + 4);
+    bf16x8 v = {f2bf(a.x), f2bf(a.y), f2bf(a.z), f2bf(a.w), f2bf(b.x), f2bf(b.y), f2bf(b.z), f2bf(b.w)};
+    return *reinterpret_cast<uint4*>(&v);
+  }
+};
+
+template <typename T> F5H_DEV constexpr int elems16() { return 16 / (int)sizeof(T); }

@@ -1,0 +1,455 @@
+// Row-wise and elementwise kernels of the CFM hot path (HBM-bound; one wave per row,
+// 16-byte vector accesses). Each cites the reference op it restates.
+#include "common.h"
+#include "kernels.h"
+
+namespace f5h {
+
+static inline unsigned nblk(int64_t n, int t) { return (unsigned)((n + t - 1) / t); }
+
+template <typename T> F5H_DEV void store4(T* p, float a, float b, float c, float d);
+template <> F5H_DEV void store4<float>(float* p, float a, float b, float c, float d) {
+  *reinterpret_cast<float4*>(p) = make_float4(a, b, c, d);
+}
+template <> F5H_DEV void store4<bf16>(bf16* p, float a, float b, float c, float d) {
+  bf16x4 v = {f2bf(a), f2bf(b), f2bf(c), f2bf(d)};
+  *reinterpret_cast<bf16x4*>(p) = v;
+}
+
+// ---------------------------------------------------------------- time embedding
+// SinusPositionEmbedding(256), scale 1000 (modules.py:157-169): [sin | cos](1000 t e^{-i ln1e4/127})
+struct TVals {
+  float t[512];
+};
+__global__ void time_sinus_kernel(TVals tv, int n, float* out) {
+  int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n * 128) return;
+  int r = i / 128, j = i % 128;
+  const float k = logf(10000.f) / 127.f;
+  float f = expf((float)j * -k);
+  float e = (1000.f * tv.t[r]) * f;
+  out[r * 256 + j] = sinf(e);
+  out[r * 256 + 128 + j] = cosf(e);
+}
+// t_host: host array of n <= 512 time values, passed by value in the kernel arguments
+// (no host->device copy, so the launch is graph-capturable).
+hipError_t time_sinus(const float* t_host, int n, float* out, hipStream_t st) {
+  if (n <= 0 || n > 512) return hipErrorInvalidValue;
+  TVals tv{};
+  for (int i = 0; i < n; ++i) tv.t[i] = t_host[i];
+  hipLaunchKernelGGL(time_sinus_kernel, dim3(nblk(n * 128, 256)), dim3(256), 0, st, tv, n, out);
+  return hipGetLastError();
+}
+
+__global__ void silu_kernel(const float* x, float* y, int64_t n) {
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) y[i] = silu(x[i]);
+}
+hipError_t silu_inplace_copy(const float* x, float* y, int64_t n, hipStream_t st) {
+  hipLaunchKernelGGL(silu_kernel, dim3(nblk(n, 256)), dim3(256), 0, st, x, y, n);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------- norms
+// One wave per row, row cached in registers (d <= 2048, d % 4 == 0).
+constexpr int MAXV = 8;  // float4 per lane
+
+// LayerNorm(no affine, eps 1e-6) * (1 + scale) + shift (AdaLayerNorm modules.py:325, ff_norm :753,
+// AdaLayerNorm_Final :346)
+template <typename TO>
+__global__ void ln_mod_kernel(const float* h, int M, int d, const float* shift, const float* scale, TO* out) {
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (row >= M) return;
+  const float4* x = reinterpret_cast<const float4*>(h + (int64_t)row * d);
+  const int n4 = d >> 2;
+  float4 v[MAXV];
+  float s = 0.f;
+#pragma unroll
+  for (int k = 0; k < MAXV; ++k) {
+    int i = lane + 64 * k;
+    v[k] = i < n4 ? x[i] : make_float4(0, 0, 0, 0);
+    s += v[k].x + v[k].y + v[k].z + v[k].w;
+  }
+  const float mean = wave_sum(s) / d;
+  float q = 0.f;
+#pragma unroll
+  for (int k = 0; k < MAXV; ++k) {
+    int i = lane + 64 * k;
+    if (i < n4) {
+      float a = v[k].x - mean, b = v[k].y - mean, c = v[k].z - mean, e = v[k].w - mean;
+      q += a * a + b * b + c * c + e * e;
+    }
+  }
+  const float rstd = rsqrtf(wave_sum(q) / d + 1e-6f);
+  const float4* sh = reinterpret_cast<const float4*>(shift);
+  const float4* sc = reinterpret_cast<const float4*>(scale);
+#pragma unroll
+  for (int k = 0; k < MAXV; ++k) {
+    int i = lane + 64 * k;
+    if (i < n4) {
+      float4 a = sc[i], b = sh[i];
+      store4<TO>(out + (int64_t)row * d + 4 * i, (v[k].x - mean) * rstd * (1.f + a.x) + b.x,
+                 (v[k].y - mean) * rstd * (1.f + a.y) + b.y, (v[k].z - mean) * rstd * (1.f + a.z) + b.z,
+                 (v[k].w - mean) * rstd * (1.f + a.w) + b.w);
+    }
+  }
+}
+hipError_t ln_modulate(int compute, const float* h, int M, int d, const float* shift, const float* scale, void* out,
+                       hipStream_t st) {
+  if (d % 4 || d > 4 * 64 * MAXV) return hipErrorInvalidValue;
+  if (compute)
+    hipLaunchKernelGGL(ln_mod_kernel<bf16>, dim3(nblk(M, 4)), dim3(256), 0, st, h, M, d, shift, scale, (bf16*)out);
+  else
+    hipLaunchKernelGGL(ln_mod_kernel<float>, dim3(nblk(M, 4)), dim3(256), 0, st, h, M, d, shift, scale, (float*)out);
+  return hipGetLastError();
+}
+
+// x_transformers RMSNorm: F.normalize(x, dim=-1) * sqrt(d) * g (unett.py:156,160,185)
+template <typename TO>
+__global__ void rms_kernel(const float* h, int M, int d, const float* g, TO* out) {
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (row >= M) return;
+  const float4* x = reinterpret_cast<const float4*>(h + (int64_t)row * d);
+  const int n4 = d >> 2;
+  float4 v[MAXV];
+  float q = 0.f;
+#pragma unroll
+  for (int k = 0; k < MAXV; ++k) {
+    int i = lane + 64 * k;
+    v[k] = i < n4 ? x[i] : make_float4(0, 0, 0, 0);
+    q += v[k].x * v[k].x + v[k].y * v[k].y + v[k].z * v[k].z + v[k].w * v[k].w;
+  }
+  const float nrm = fmaxf(sqrtf(wave_sum(q)), 1e-12f);
+  const float f = sqrtf((float)d);
+  const float4* gg = reinterpret_cast<const float4*>(g);
+#pragma unroll
+  for (int k = 0; k < MAXV; ++k) {
+    int i = lane + 64 * k;
+    if (i < n4) {
+      float4 a = gg[i];
+      store4<TO>(out + (int64_t)row * d + 4 * i, v[k].x / nrm * f * a.x, v[k].y / nrm * f * a.y,
+                 v[k].z / nrm * f * a.z, v[k].w / nrm * f * a.w);
+    }
+  }
+}
+hipError_t rms_norm_g(int compute, const float* h, int M, int d, const float* g, void* out, hipStream_t st) {
+  if (d % 4 || d > 4 * 64 * MAXV) return hipErrorInvalidValue;
+  if (compute)
+    hipLaunchKernelGGL(rms_kernel<bf16>, dim3(nblk(M, 4)), dim3(256), 0, st, h, M, d, g, (bf16*)out);
+  else
+    hipLaunchKernelGGL(rms_kernel<float>, dim3(nblk(M, 4)), dim3(256), 0, st, h, M, d, g, (float*)out);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------- rotary table
+// x_transformers RotaryEmbedding(64): inv_freq_j = 1/10000^(2j/64), freqs[n,2j]=freqs[n,2j+1]=n*inv_freq_j
+__global__ void rope_kernel(int L, float2* out) {
+  int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= L * 32) return;
+  int pos = i >> 5, j = i & 31;
+  float inv = 1.f / powf(10000.f, (float)(2 * j) / 64.f);
+  float f = (float)pos * inv;
+  out[i] = make_float2(cosf(f), sinf(f));
+}
+hipError_t rope_table(int L, float2* out, hipStream_t st) {
+  hipLaunchKernelGGL(rope_kernel, dim3(nblk(L * 32, 256)), dim3(256), 0, st, L, out);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------- text embedding
+// TextEmbedding.forward (dit.py:86-120): tok+1 (filler 0), truncate/pad to N, per-sample
+// valid mask (batched path), fill mask taken BEFORE drop_text, Embedding, + freqs_cis, masked_fill.
+__global__ void text_embed_kernel(TextEmbArgs a) {
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (row >= a.B * a.N) return;
+  const int b = row / a.N, n = row - b * a.N;
+  const bool valid = !a.seq_len || n < a.seq_len[b];
+  int tok = n < a.nt ? (int)a.text[(int64_t)b * a.nt + n] + 1 : 0;
+  if (!valid) tok = 0;
+  const bool fill = tok == 0;
+  const bool zero_row = a.mask_padding && a.freqs && fill;  // masked_fill only with extra modeling
+  if (a.keep && lane == 0) {
+    a.keep[row] = zero_row ? 0 : 1;
+    a.keep[a.B * a.N + row] = zero_row ? 0 : 1;
+  }
+  for (int c = lane; c < a.td; c += 64) {
+    float ec = valid ? a.table[(int64_t)tok * a.td + c] : 0.f;
+    float eu = valid ? a.table[c] : 0.f;  // drop_text -> id 0
+    if (a.freqs) {
+      float f = valid ? a.freqs[(int64_t)n * a.td + c] : 0.f;
+      ec += f;
+      eu += f;
+    }
+    if (zero_row) ec = eu = 0.f;
+    a.out_c[(int64_t)row * a.td + c] = ec;
+    a.out_u[(int64_t)row * a.td + c] = eu;
+  }
+}
+hipError_t text_embed(const TextEmbArgs& a, hipStream_t st) {
+  hipLaunchKernelGGL(text_embed_kernel, dim3(nblk((int64_t)a.B * a.N, 4)), dim3(256), 0, st, a);
+  return hipGetLastError();
+}
+
+// ConvNeXtV2Block front half (modules.py:260-264): depthwise Conv1d(k7, pad3) + bias -> LayerNorm(affine)
+template <typename TO>
+__global__ void dwconv_ln_kernel(const float* x, int S, int L, int C, const float* w, const float* bias,
+                                 const float* lw, const float* lb, TO* out) {
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (row >= S * L) return;
+  const int s = row / L, n = row - s * L;
+  float v[16];  // C <= 1024
+  float sum = 0.f;
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    int c = lane + 64 * k;
+    float acc = 0.f;
+    if (c < C) {
+      acc = bias[c];
+#pragma unroll
+      for (int t = 0; t < 7; ++t) {
+        int q = n + t - 3;
+        if (q >= 0 && q < L) acc += w[c * 7 + t] * x[((int64_t)s * L + q) * C + c];
+      }
+    }
+    v[k] = acc;
+    sum += acc;
+  }
+  const float mean = wave_sum(sum) / C;
+  float q2 = 0.f;
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    int c = lane + 64 * k;
+    if (c < C) q2 += (v[k] - mean) * (v[k] - mean);
+  }
+  const float rstd = rsqrtf(wave_sum(q2) / C + 1e-6f);
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    int c = lane + 64 * k;
+    if (c < C) out[(int64_t)row * C + c] = from_f32<TO>((v[k] - mean) * rstd * lw[c] + lb[c]);
+  }
+}
+hipError_t dwconv_ln(int compute, const float* x, int S, int L, int C, const float* dw_w, const float* dw_b,
+                     const float* ln_w, const float* ln_b, void* out, hipStream_t st) {
+  if (C > 1024) return hipErrorInvalidValue;
+  if (compute)
+    hipLaunchKernelGGL(dwconv_ln_kernel<bf16>, dim3(nblk(S * L, 4)), dim3(256), 0, st, x, S, L, C, dw_w, dw_b, ln_w,
+                       ln_b, (bf16*)out);
+  else
+    hipLaunchKernelGGL(dwconv_ln_kernel<float>, dim3(nblk(S * L, 4)), dim3(256), 0, st, x, S, L, C, dw_w, dw_b,
+                       ln_w, ln_b, (float*)out);
+  return hipGetLastError();
+}
+
+// GRN (modules.py:236-245): Gx = ||x||_2 over the TIME axis, Nx = Gx / (mean_c Gx + 1e-6),
+// out = gamma * (x * Nx) + beta + x
+__global__ void grn_sumsq_kernel(const float* x, int L, int C, float* sumsq) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x, s = blockIdx.y;
+  if (c >= C) return;
+  float acc = 0.f;
+  for (int n = 0; n < L; ++n) {
+    float v = x[((int64_t)s * L + n) * C + c];
+    acc += v * v;
+  }
+  sumsq[(int64_t)s * C + c] = sqrtf(acc);
+}
+__global__ void grn_norm_kernel(float* gx, int C) {
+  const int s = blockIdx.x;
+  float acc = 0.f;
+  for (int c = threadIdx.x; c < C; c += 256) acc += gx[(int64_t)s * C + c];
+  __shared__ float red[4];
+  acc = wave_sum(acc);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
+  __syncthreads();
+  const float mean = (red[0] + red[1] + red[2] + red[3]) / C;
+  for (int c = threadIdx.x; c < C; c += 256) gx[(int64_t)s * C + c] = gx[(int64_t)s * C + c] / (mean + 1e-6f);
+}
+template <typename TO>
+__global__ void grn_apply_kernel(const float* x, int L, int C, const float* nx, const float* gamma,
+                                 const float* beta, TO* out, int64_t total) {
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= total) return;
+  int c = (int)(i % C);
+  int s = (int)(i / ((int64_t)L * C));
+  float v = x[i];
+  out[i] = from_f32<TO>(gamma[c] * (v * nx[(int64_t)s * C + c]) + beta[c] + v);
+}
+hipError_t grn(int compute, const float* x, int S, int L, int C, const float* gamma, const float* beta,
+               float* scratch, void* out, hipStream_t st) {
+  hipLaunchKernelGGL(grn_sumsq_kernel, dim3(nblk(C, 256), S), dim3(256), 0, st, x, L, C, scratch);
+  hipLaunchKernelGGL(grn_norm_kernel, dim3(S), dim3(256), 0, st, scratch, C);
+  const int64_t total = (int64_t)S * L * C;
+  if (compute)
+    hipLaunchKernelGGL(grn_apply_kernel<bf16>, dim3(nblk(total, 256)), dim3(256), 0, st, x, L, C, scratch, gamma,
+                       beta, (bf16*)out, total);
+  else
+    hipLaunchKernelGGL(grn_apply_kernel<float>, dim3(nblk(total, 256)), dim3(256), 0, st, x, L, C, scratch, gamma,
+                       beta, (float*)out, total);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------- input-projection operands
+// A_ct row (s, n) = [step_cond (or 0 for the uncond branch, dit.py:155-156) pad->128 | text_e pad->tdp]
+template <typename TO>
+__global__ void build_ct_kernel(const float* cond, const uint8_t* cmask, const float* tc, const float* tu, int B,
+                                int N, int td, int tdp, int S, TO* out) {
+  const int64_t K = 128 + tdp;
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (int64_t)S * N * K) return;
+  const int64_t row = i / K;
+  const int col = (int)(i - row * K);
+  const int s = (int)(row / N), n = (int)(row - (int64_t)s * N);
+  const int b = s % B;
+  float v = 0.f;
+  if (col < 128) {
+    if (col < 100 && s < B && cmask[(int64_t)b * N + n]) v = cond[((int64_t)b * N + n) * 100 + col];
+  } else if (col - 128 < td) {
+    const float* t = s < B ? tc : tu;
+    v = t[((int64_t)b * N + n) * td + (col - 128)];
+  }
+  out[i] = from_f32<TO>(v);
+}
+hipError_t build_ct(int compute, const float* cond, const uint8_t* cond_mask, const float* text_c,
+                    const float* text_u, int B, int N, int td, int S, void* out, hipStream_t st) {
+  const int tdp = (td + 63) / 64 * 64;
+  const int64_t total = (int64_t)S * N * (128 + tdp);
+  if (compute)
+    hipLaunchKernelGGL(build_ct_kernel<bf16>, dim3(nblk(total, 256)), dim3(256), 0, st, cond, cond_mask, text_c,
+                       text_u, B, N, td, tdp, S, (bf16*)out);
+  else
+    hipLaunchKernelGGL(build_ct_kernel<float>, dim3(nblk(total, 256)), dim3(256), 0, st, cond, cond_mask, text_c,
+                       text_u, B, N, td, tdp, S, (float*)out);
+  return hipGetLastError();
+}
+
+template <typename TO>
+__global__ void pack_y_kernel(const float* y, int rows, int mel, TO* yp) {
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (int64_t)rows * 128) return;
+  int64_t r = i >> 7;
+  int c = (int)(i & 127);
+  yp[i] = from_f32<TO>(c < mel ? y[r * mel + c] : 0.f);
+}
+hipError_t pack_y(int compute, const float* y, int rows, int mel, void* ypad, hipStream_t st) {
+  const int64_t total = (int64_t)rows * 128;
+  if (compute)
+    hipLaunchKernelGGL(pack_y_kernel<bf16>, dim3(nblk(total, 256)), dim3(256), 0, st, y, rows, mel, (bf16*)ypad);
+  else
+    hipLaunchKernelGGL(pack_y_kernel<float>, dim3(nblk(total, 256)), dim3(256), 0, st, y, rows, mel, (float*)ypad);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------- CFG + Euler update
+// fn(t,x) = pred + (pred - null_pred) * cfg (cfm.py:190-191); torchdiffeq euler: y1 = y0 + dt * f
+template <typename TO>
+__global__ void cfg_euler_kernel(EulerArgs a, TO* ypad) {
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t total = (int64_t)a.B * a.N * a.mel;
+  if (i >= total) return;
+  const int c = (int)(i % a.mel);
+  const int64_t bn = i / a.mel;
+  const int b = (int)(bn / a.N), n = (int)(bn - (int64_t)b * a.N);
+  const float pc = a.p[(int64_t)b * a.p_seq_stride + (int64_t)(a.p_row_off + n) * a.p_ld + c];
+  float v = pc;
+  if (a.use_cfg) {
+    const float pu = a.p[(int64_t)(a.B + b) * a.p_seq_stride + (int64_t)(a.p_row_off + n) * a.p_ld + c];
+    v = __fadd_rn(pc, __fmul_rn(__fsub_rn(pc, pu), a.cfg));
+  }
+  const float y = __fadd_rn(a.y[i], __fmul_rn(a.dt, v));
+  a.y[i] = y;
+  if (ypad) ypad[bn * 128 + c] = from_f32<TO>(y);
+  if (a.traj) a.traj[i] = y;
+}
+hipError_t cfg_euler(const EulerArgs& a, hipStream_t st) {
+  const int64_t total = (int64_t)a.B * a.N * a.mel;
+  if (a.compute)
+    hipLaunchKernelGGL(cfg_euler_kernel<bf16>, dim3(nblk(total, 256)), dim3(256), 0, st, a, (bf16*)a.ypad);
+  else
+    hipLaunchKernelGGL(cfg_euler_kernel<float>, dim3(nblk(total, 256)), dim3(256), 0, st, a, (float*)a.ypad);
+  return hipGetLastError();
+}
+
+// out = where(cond_mask, cond, out) (cfm.py:223)
+__global__ void final_where_kernel(const float* cond, const uint8_t* m, float* y, int64_t total, int mel) {
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= total) return;
+  if (m[i / mel]) y[i] = cond[i];
+}
+hipError_t final_where(const float* cond, const uint8_t* cond_mask, float* y, int B, int N, int mel,
+                       hipStream_t st) {
+  const int64_t total = (int64_t)B * N * mel;
+  hipLaunchKernelGGL(final_where_kernel, dim3(nblk(total, 256)), dim3(256), 0, st, cond, cond_mask, y, total, mel);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------- masks
+__global__ void rowkeep_kernel(const int32_t* dur, int B, int S, int L, int off, uint8_t* keep) {
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (int64_t)S * L) return;
+  int s = (int)(i / L), pos = (int)(i - (int64_t)s * L);
+  keep[i] = (pos < off || pos - off < dur[s % B]) ? 1 : 0;
+}
+hipError_t build_rowkeep(const int32_t* dur, int B, int S, int L, int off, uint8_t* keep, hipStream_t st) {
+  hipLaunchKernelGGL(rowkeep_kernel, dim3(nblk((int64_t)S * L, 256)), dim3(256), 0, st, dur, B, S, L, off, keep);
+  return hipGetLastError();
+}
+__global__ void kvlen_kernel(const int32_t* dur, int B, int S, int off, int32_t* kv) {
+  int s = blockIdx.x * blockDim.x + threadIdx.x;
+  if (s < S) kv[s] = dur[s % B] + off;
+}
+hipError_t build_kvlen(const int32_t* dur, int B, int S, int off, int32_t* kv, hipStream_t st) {
+  hipLaunchKernelGGL(kvlen_kernel, dim3(nblk(S, 64)), dim3(64), 0, st, dur, B, S, off, kv);
+  return hipGetLastError();
+}
+
+__global__ void time_token_kernel(const float* temb, int S, int L, int d, float* h) {
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (int64_t)S * d) return;
+  int s = (int)(i / d), c = (int)(i % d);
+  h[(int64_t)s * L * d + c] = temb[c];
+}
+hipError_t write_time_token(const float* temb, int S, int L, int d, float* h, hipStream_t st) {
+  hipLaunchKernelGGL(time_token_kernel, dim3(nblk((int64_t)S * d, 256)), dim3(256), 0, st, temb, S, L, d, h);
+  return hipGetLastError();
+}
+
+__global__ void copy_pred_kernel(const float* p, int S, int L, int off, int mel, int64_t ld, float* dst) {
+  const int Lo = L - off;
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (int64_t)S * Lo * mel) return;
+  int c = (int)(i % mel);
+  int64_t r = i / mel;
+  int s = (int)(r / Lo), n = (int)(r - (int64_t)s * Lo);
+  dst[i] = p[((int64_t)s * L + off + n) * ld + c];
+}
+hipError_t copy_pred(const float* p, int S, int L, int row_off, int mel, int64_t p_ld, float* dst, hipStream_t st) {
+  const int64_t total = (int64_t)S * (L - row_off) * mel;
+  hipLaunchKernelGGL(copy_pred_kernel, dim3(nblk(total, 256)), dim3(256), 0, st, p, S, L, row_off, mel, p_ld, dst);
+  return hipGetLastError();
+}
+
+template <typename TO>
+__global__ void cvt_kernel(const float* x, int64_t n, TO* y) {
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) y[i] = from_f32<TO>(x[i]);
+}
+template <typename TI>
+__global__ void cvt_back_kernel(const TI* x, int64_t n, float* y) {
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) y[i] = to_f32(x[i]);
+}
+hipError_t f32_to_op(int compute, const float* x, int64_t n, void* out, hipStream_t st) {
+  if (compute)
+    hipLaunchKernelGGL(cvt_kernel<bf16>, dim3(nblk(n, 256)), dim3(256), 0, st, x, n, (bf16*)out);
+  else
+    hipLaunchKernelGGL(cvt_kernel<float>, dim3(nblk(n, 256)), dim3(256), 0, st, x, n, (float*)out);
+  return hipGetLastError();
+}
+hipError_t op_to_f32(int compute, const void* x, int64_t n, float* out, hipStream_t st) {
+  if (compute)
+    hipLaunchKernelGGL(cvt_back_kernel<bf16>, dim3(nblk(n, 256)), dim3(256), 0, st, (const bf16*)x, n, out);
+  else
+    hipLaunchKernelGGL(cvt_back_kernel<float>, dim3(nblk(n, 256)), dim3(256), 0, st, (const float*)x, n, out);
+  return hipGetLastError();
+}
+
+}  // namespace f5h

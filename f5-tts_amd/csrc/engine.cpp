@@ -1,0 +1,876 @@
+// f5h engine: weight packing, workspace layout and the CFM.sample orchestration behind the
+// C ABI declared in include/f5h.h. Host code; every kernel is enqueued on the caller's stream.
+//
+// Hot-path map (reference file:line -> what runs here):
+//   cfm.py:211-216  t grid            -> host (caller), passed as t_grid
+//   modules.py:852-862, 321-323, 342-344  time MLP + every AdaLN row for every step
+//                                     -> three GEMMs before the loop (one table [nfe, depth*6d+2d])
+//   dit.py:86-139 text embed (cached) -> text_embed + ConvNeXt kernels once per call (both branches)
+//   dit.py:159-162 InputEmbedding.proj -> split: cond/text part hoisted (P), x part per step
+//   modules.py:175-201 ConvPositionEmbedding -> conv_pos x2 (implicit-GEMM MFMA)
+//   modules.py:743-757 DiTBlock x depth -> ln_modulate, QKV+RoPE GEMM, attention, out GEMM+gate,
+//                                     ln_modulate, FFN1+GELU GEMM, FFN2 GEMM+gate
+//   dit.py:367-368, cfm.py:190-191, torchdiffeq euler -> ln_modulate, proj_out GEMM, cfg_euler
+//   cfm.py:223 final where            -> final_where
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "../../include/f5h.h"
+#include "kernels.h"
+
+using namespace f5h;
+
+static thread_local std::string g_err;
+static int fail(int code, const std::string& msg) {
+  g_err = msg;
+  return code;
+}
+#define HIPCK(x)                                                                               \
+  do {                                                                                         \
+    hipError_t _e = (x);                                                                       \
+    if (_e != hipSuccess) return fail(F5H_EHIP, std::string(#x) + ": " + hipGetErrorString(_e)); \
+  } while (0)
+
+#define RC(x)              \
+  do {                     \
+    int _r = (x);          \
+    if (_r) return _r;     \
+  } while (0)
+
+static uint16_t f2bf_host(float f) {
+  uint32_t u;
+  std::memcpy(&u, &f, 4);
+  if ((u & 0x7fffffffu) > 0x7f800000u) return (uint16_t)((u >> 16) | 0x40);
+  u += 0x7fffu + ((u >> 16) & 1u);
+  return (uint16_t)(u >> 16);
+}
+
+struct Lin {
+  void* w = nullptr;      // [Npad][K] operand dtype
+  float* b = nullptr;     // [Npad] fp32 (may be null)
+  int N = 0, K = 0, Npad = 0;
+};
+
+struct CNX {
+  float *dw_w = nullptr, *dw_b = nullptr, *ln_w = nullptr, *ln_b = nullptr, *gamma = nullptr, *beta = nullptr;
+  Lin pw1, pw2;
+};
+
+struct Layer {
+  Lin qkv, out, ff1, ff2, skip1, skip2;
+  float *g_attn = nullptr, *g_ff = nullptr;  // UNetT RMSNorm gains
+};
+
+struct f5h_engine {
+  f5h_arch a{};
+  int dev = 0;
+  int bf = 0;          // compute == BF16
+  size_t esz = 4;      // operand element size
+  int tdp = 0;         // text_dim padded to 64
+  std::vector<void*> allocs;
+  Lin t1, t2, ada, in_x, in_ct, proj_out;
+  float* text_table = nullptr;
+  float* freqs = nullptr;
+  std::vector<CNX> cnx;
+  void* conv_w[2] = {nullptr, nullptr};
+  float* conv_b[2] = {nullptr, nullptr};
+  std::vector<Layer> layers;
+  float* norm_out_g = nullptr;
+  // probe
+  std::mutex pm;
+  int probe_class = -1;
+  std::vector<hipEvent_t> ev;  // pairs
+  size_t ev_used = 0;
+  int64_t probe_launches = 0;
+  double probe_ms = 0.0;
+};
+
+// ---------------------------------------------------------------- weight packing
+struct WMap {
+  std::unordered_map<std::string, std::pair<const float*, int64_t>> m;
+  const float* get(const std::string& n, int64_t numel, std::string* err) const {
+    auto it = m.find(n);
+    if (it == m.end()) {
+      *err = "missing weight " + n;
+      return nullptr;
+    }
+    if (it->second.second != numel) {
+      *err = "weight " + n + " has " + std::to_string(it->second.second) + " elements, expected " +
+             std::to_string(numel);
+      return nullptr;
+    }
+    return it->second.first;
+  }
+};
+
+template <typename T>
+static int upload(f5h_engine* e, const std::vector<T>& h, T** out) {
+  void* p = nullptr;
+  HIPCK(hipMalloc(&p, h.size() * sizeof(T) + 16));
+  e->allocs.push_back(p);
+  HIPCK(hipMemcpy(p, h.data(), h.size() * sizeof(T), hipMemcpyHostToDevice));
+  *out = reinterpret_cast<T*>(p);
+  return 0;
+}
+
+static int upload_op(f5h_engine* e, const std::vector<float>& h, void** out) {
+  if (e->bf) {
+    std::vector<uint16_t> b(h.size());
+    for (size_t i = 0; i < h.size(); ++i) b[i] = f2bf_host(h[i]);
+    uint16_t* p;
+    int rc = upload(e, b, &p);
+    *out = p;
+    return rc;
+  }
+  float* p;
+  int rc = upload(e, h, &p);
+  *out = p;
+  return rc;
+}
+
+// Upload a host panel [Npad][K] (+ optional bias [N]) as a GEMM weight.
+static int lin_from_host(f5h_engine* e, const std::vector<float>& w, int N, int K, const std::vector<float>* bias,
+                         Lin* L) {
+  L->N = N;
+  L->K = K;
+  L->Npad = (N + 127) / 128 * 128;
+  RC(upload_op(e, w, &L->w));
+  if (bias) {
+    std::vector<float> bv(L->Npad, 0.f);
+    std::copy(bias->begin(), bias->end(), bv.begin());
+    RC(upload(e, bv, &L->b));
+  }
+  return 0;
+}
+
+// Build a GEMM panel from column blocks of several source matrices stacked along N.
+struct Block {
+  const float* src;   // [rows][ld]
+  int rows, ld, col0, ncols, dst_col;
+};
+static int make_lin(f5h_engine* e, const std::vector<Block>& blocks, int K, const std::vector<const float*>& biases,
+                    const std::vector<int>& bias_rows, Lin* L) {
+  int N = 0;
+  std::vector<int> row0(blocks.size());
+  for (size_t i = 0; i < blocks.size(); ++i) {
+    row0[i] = N;
+    N += blocks[i].rows;
+  }
+  const int Npad = (N + 127) / 128 * 128;
+  std::vector<float> w((size_t)Npad * K, 0.f);
+  for (size_t i = 0; i < blocks.size(); ++i) {
+    const Block& b = blocks[i];
+    for (int r = 0; r < b.rows; ++r)
+      for (int c = 0; c < b.ncols; ++c)
+        w[(size_t)(row0[i] + r) * K + b.dst_col + c] = b.src[(size_t)r * b.ld + b.col0 + c];
+  }
+  if (biases.empty()) return lin_from_host(e, w, N, K, nullptr, L);
+  std::vector<float> bv;
+  for (size_t i = 0; i < biases.size(); ++i)
+    for (int r = 0; r < bias_rows[i]; ++r) bv.push_back(biases[i] ? biases[i][r] : 0.f);
+  return lin_from_host(e, w, N, K, &bv, L);
+}
+// Simple linear: weight [N][K] (K padded to Kp), bias [N] or null.
+static int lin_simple(f5h_engine* e, const WMap& W, const std::string& wn, const std::string& bn, int N, int K,
+                      Lin* L, std::string* err) {
+  const float* w = W.get(wn, (int64_t)N * K, err);
+  if (!w) return fail(F5H_ENOWEIGHT, *err);
+  const float* b = nullptr;
+  if (!bn.empty()) {
+    b = W.get(bn, N, err);
+    if (!b) return fail(F5H_ENOWEIGHT, *err);
+  }
+  const int Kp = (K + 63) / 64 * 64;
+  return make_lin(e, {Block{w, N, K, 0, K, 0}}, Kp, b ? std::vector<const float*>{b} : std::vector<const float*>{},
+                  std::vector<int>{N}, L);
+}
+static int vec_upload(f5h_engine* e, const WMap& W, const std::string& n, int64_t numel, float** out, std::string* err) {
+  const float* p = W.get(n, numel, err);
+  if (!p) return fail(F5H_ENOWEIGHT, *err);
+  return upload(e, std::vector<float>(p, p + numel), out);
+}
+
+
+static int pack_all(f5h_engine* e, const WMap& W) {
+  const f5h_arch& a = e->a;
+  const int d = a.dim, inner = a.heads * a.dim_head, F = a.ff_dim, td = a.text_dim, mel = a.mel_dim;
+  const int V = a.text_num_embeds + 1;
+  std::string err;
+  // time MLP (modules.py:852-862)
+  RC(lin_simple(e, W, "time_embed.time_mlp.0.weight", "time_embed.time_mlp.0.bias", d, 256, &e->t1, &err));
+  RC(lin_simple(e, W, "time_embed.time_mlp.2.weight", "time_embed.time_mlp.2.bias", d, d, &e->t2, &err));
+  // text table
+  RC(vec_upload(e, W, "text_embed.text_embed.weight", (int64_t)V * td, &e->text_table, &err));
+  if (a.conv_layers > 0) {
+    // precompute_freqs_cis(text_dim, 8192) (modules.py:207-218)
+    std::vector<float> fc((size_t)8192 * td);
+    const int half = td / 2;
+    for (int p = 0; p < 8192; ++p)
+      for (int i = 0; i < half; ++i) {
+        float f = 1.0f / std::pow(10000.0f, (float)(2 * i) / (float)td);
+        float ang = (float)p * f;
+        fc[(size_t)p * td + i] = std::cos(ang);
+        fc[(size_t)p * td + half + i] = std::sin(ang);
+      }
+    RC(upload(e, fc, &e->freqs));
+  }
+  e->cnx.resize(a.conv_layers);
+  for (int i = 0; i < a.conv_layers; ++i) {
+    const std::string p = "text_embed.text_blocks." + std::to_string(i) + ".";
+    CNX& c = e->cnx[i];
+    RC(vec_upload(e, W, p + "dwconv.weight", (int64_t)td * 7, &c.dw_w, &err));
+    RC(vec_upload(e, W, p + "dwconv.bias", td, &c.dw_b, &err));
+    RC(vec_upload(e, W, p + "norm.weight", td, &c.ln_w, &err));
+    RC(vec_upload(e, W, p + "norm.bias", td, &c.ln_b, &err));
+    RC(vec_upload(e, W, p + "grn.gamma", 2 * td, &c.gamma, &err));
+    RC(vec_upload(e, W, p + "grn.beta", 2 * td, &c.beta, &err));
+    RC(lin_simple(e, W, p + "pwconv1.weight", p + "pwconv1.bias", 2 * td, td, &c.pw1, &err));
+    RC(lin_simple(e, W, p + "pwconv2.weight", p + "pwconv2.bias", td, 2 * td, &c.pw2, &err));
+  }
+  // input projection split (dit.py:162): [x | cond | text] -> x part per step, cond|text hoisted
+  {
+    const int Kin = 2 * mel + td;
+    const float* w = W.get("input_embed.proj.weight", (int64_t)d * Kin, &err);
+    const float* b = W.get("input_embed.proj.bias", d, &err);
+    if (!w || !b) return fail(F5H_ENOWEIGHT, err);
+    RC(make_lin(e, {Block{w, d, Kin, 0, mel, 0}}, 128, {}, {d}, &e->in_x));
+    // cond columns -> [0,128), text columns -> [128, 128+tdp)
+    const int Kct = 128 + e->tdp;
+    std::vector<float> tmp((size_t)((d + 127) / 128 * 128) * Kct, 0.f);
+    for (int r = 0; r < d; ++r) {
+      for (int c = 0; c < mel; ++c) tmp[(size_t)r * Kct + c] = w[(size_t)r * Kin + mel + c];
+      for (int c = 0; c < td; ++c) tmp[(size_t)r * Kct + 128 + c] = w[(size_t)r * Kin + 2 * mel + c];
+    }
+    std::vector<float> bv(b, b + d);
+    RC(lin_from_host(e, tmp, d, Kct, &bv, &e->in_ct));
+  }
+  // ConvPositionEmbedding: [d, d/16, 31] -> [16][31][64 out][64 in] (zero-padded to 64 channels)
+  for (int j = 0; j < 2; ++j) {
+    const std::string p = "input_embed.conv_pos_embed.conv1d." + std::to_string(j * 2) + ".";
+    const int cg = d / 16;
+    const float* w = W.get(p + "weight", (int64_t)d * cg * 31, &err);
+    if (!w) return fail(F5H_ENOWEIGHT, err);
+    std::vector<float> pk((size_t)16 * 31 * 64 * 64, 0.f);
+    for (int g = 0; g < 16; ++g)
+      for (int o = 0; o < cg; ++o)
+        for (int i = 0; i < cg; ++i)
+          for (int t = 0; t < 31; ++t)
+            pk[(((size_t)g * 31 + t) * 64 + o) * 64 + i] = w[((size_t)(g * cg + o) * cg + i) * 31 + t];
+    RC(upload_op(e, pk, &e->conv_w[j]));
+    RC(vec_upload(e, W, p + "bias", d, &e->conv_b[j], &err));
+  }
+  // blocks
+  e->layers.resize(a.depth);
+  std::vector<Block> ada_blocks;
+  std::vector<const float*> ada_bias;
+  std::vector<int> ada_rows;
+  for (int l = 0; l < a.depth; ++l) {
+    Layer& L = e->layers[l];
+    const bool dit = a.backbone == F5H_DIT;
+    const std::string p = dit ? "transformer_blocks." + std::to_string(l) + "." : "layers." + std::to_string(l) + ".";
+    const std::string pa = dit ? p + "attn." : p + "2.";
+    const std::string pf = dit ? p + "ff.ff." : p + "4.ff.";
+    const float *wq = W.get(pa + "to_q.weight", (int64_t)inner * d, &err), *wk = W.get(pa + "to_k.weight", (int64_t)inner * d, &err),
+                *wv = W.get(pa + "to_v.weight", (int64_t)inner * d, &err);
+    const float *bq = W.get(pa + "to_q.bias", inner, &err), *bk = W.get(pa + "to_k.bias", inner, &err),
+                *bv = W.get(pa + "to_v.bias", inner, &err);
+    if (!wq || !wk || !wv || !bq || !bk || !bv) return fail(F5H_ENOWEIGHT, err);
+    RC(make_lin(e, {Block{wq, inner, d, 0, d, 0}, Block{wk, inner, d, 0, d, 0}, Block{wv, inner, d, 0, d, 0}}, d,
+                {bq, bk, bv}, {inner, inner, inner}, &L.qkv));
+    RC(lin_simple(e, W, pa + "to_out.0.weight", pa + "to_out.0.bias", d, inner, &L.out, &err));
+    RC(lin_simple(e, W, pf + "0.0.weight", pf + "0.0.bias", F, d, &L.ff1, &err));
+    RC(lin_simple(e, W, pf + "2.weight", pf + "2.bias", d, F, &L.ff2, &err));
+    if (dit) {
+      const float* aw = W.get(p + "attn_norm.linear.weight", (int64_t)6 * d * d, &err);
+      const float* ab = W.get(p + "attn_norm.linear.bias", 6 * d, &err);
+      if (!aw || !ab) return fail(F5H_ENOWEIGHT, err);
+      ada_blocks.push_back(Block{aw, 6 * d, d, 0, d, 0});
+      ada_bias.push_back(ab);
+      ada_rows.push_back(6 * d);
+    } else {
+      RC(vec_upload(e, W, p + "1.g", d, &L.g_attn, &err));
+      RC(vec_upload(e, W, p + "3.g", d, &L.g_ff, &err));
+      if (l >= a.depth / 2) {
+        const float* sw = W.get(p + "0.weight", (int64_t)d * 2 * d, &err);
+        if (!sw) return fail(F5H_ENOWEIGHT, err);
+        RC(make_lin(e, {Block{sw, d, 2 * d, 0, d, 0}}, d, {}, {d}, &L.skip1));
+        RC(make_lin(e, {Block{sw, d, 2 * d, d, d, 0}}, d, {}, {d}, &L.skip2));
+      }
+    }
+  }
+  if (a.backbone == F5H_DIT) {
+    const float* nw = W.get("norm_out.linear.weight", (int64_t)2 * d * d, &err);
+    const float* nb = W.get("norm_out.linear.bias", 2 * d, &err);
+    if (!nw || !nb) return fail(F5H_ENOWEIGHT, err);
+    ada_blocks.push_back(Block{nw, 2 * d, d, 0, d, 0});
+    ada_bias.push_back(nb);
+    ada_rows.push_back(2 * d);
+    RC(make_lin(e, ada_blocks, d, ada_bias, ada_rows, &e->ada));
+  } else {
+    RC(vec_upload(e, W, "norm_out.g", d, &e->norm_out_g, &err));
+  }
+  RC(lin_simple(e, W, "proj_out.weight", "proj_out.bias", mel, d, &e->proj_out, &err));
+  return 0;
+}
+
+// ---------------------------------------------------------------- workspace layout
+struct WS {
+  size_t off = 0;
+  char* base = nullptr;
+  template <typename T>
+  T* take(size_t n) {
+    size_t o = off;
+    off = (off + n * sizeof(T) + 255) / 256 * 256;
+    return base ? reinterpret_cast<T*>(base + o) : nullptr;
+  }
+};
+
+struct Bufs {
+  float *tsin, *th, *temb, *tsilu, *ada;
+  float *te, *pw1o, *grn_scr;
+  void *dwln, *grno;
+  uint8_t* keepfill;
+  void* act;
+  float* P;
+  void* ypad;
+  float *h0, *h, *h2, *p;
+  void *c1, *aop, *q, *k, *v, *o, *f;
+  float2* rope;
+  uint8_t* rowkeep;
+  int32_t* kvlen;
+  std::vector<float*> skips;
+};
+
+static void layout(const f5h_engine* e, WS& ws, Bufs& b, int B, int N, int nfe, int use_cfg) {
+  const f5h_arch& a = e->a;
+  const int d = a.dim, td = a.text_dim, S = use_cfg ? 2 * B : B;
+  const int L = a.backbone == F5H_DIT ? N : N + 1;
+  const size_t rows = (size_t)S * L, es = e->esz;
+  const int inner = a.heads * 64;
+  b.tsin = ws.take<float>((size_t)nfe * 256);
+  b.th = ws.take<float>((size_t)nfe * d);
+  b.temb = ws.take<float>((size_t)nfe * d);
+  b.tsilu = ws.take<float>((size_t)nfe * d);
+  b.ada = a.backbone == F5H_DIT ? ws.take<float>((size_t)nfe * e->ada.Npad) : nullptr;
+  b.te = ws.take<float>((size_t)2 * B * N * td);
+  b.keepfill = ws.take<uint8_t>((size_t)2 * B * N);
+  if (a.conv_layers > 0) {
+    b.dwln = ws.take<char>((size_t)2 * B * N * td * es);
+    b.pw1o = ws.take<float>((size_t)2 * B * N * 2 * td);
+    b.grno = ws.take<char>((size_t)2 * B * N * 2 * td * es);
+    b.grn_scr = ws.take<float>((size_t)2 * B * 2 * td);
+  } else {
+    b.dwln = b.grno = nullptr;
+    b.pw1o = b.grn_scr = nullptr;
+  }
+  b.act = ws.take<char>((size_t)S * N * (128 + e->tdp) * es);
+  b.P = ws.take<float>((size_t)S * N * d);
+  b.ypad = ws.take<char>((size_t)B * N * 128 * es);
+  b.h0 = ws.take<float>((size_t)S * N * d);
+  b.c1 = ws.take<char>((size_t)S * N * d * es);
+  b.h = ws.take<float>(rows * d);
+  b.h2 = a.backbone == F5H_UNETT ? ws.take<float>(rows * d) : nullptr;
+  b.aop = ws.take<char>(rows * d * es);
+  b.q = ws.take<char>(rows * inner * es);
+  b.k = ws.take<char>(rows * inner * es);
+  b.v = ws.take<char>(rows * inner * es);
+  b.o = ws.take<char>(rows * inner * es);
+  b.f = ws.take<char>(rows * a.ff_dim * es);
+  b.p = ws.take<float>(rows * a.mel_dim);
+  b.rope = ws.take<float2>((size_t)L * 32);
+  b.rowkeep = ws.take<uint8_t>(rows);
+  b.kvlen = ws.take<int32_t>(S);
+  b.skips.clear();
+  if (a.backbone == F5H_UNETT)
+    for (int i = 0; i < a.depth / 2; ++i) b.skips.push_back(ws.take<float>(rows * d));
+}
+
+// ---------------------------------------------------------------- probe
+enum { KC_FFN1 = 0, KC_ATTN = 1, KC_QKV = 2, KC_FFN2 = 3, KC_CONV = 4 };
+struct ProbeScope {
+  f5h_engine* e;
+  hipStream_t st;
+  bool on;
+  size_t idx = 0;
+  ProbeScope(f5h_engine* e_, int kc, hipStream_t s) : e(e_), st(s), on(e_->probe_class == kc) {
+    if (on) {
+      std::lock_guard<std::mutex> g(e->pm);
+      if (e->ev_used + 2 > e->ev.size()) {
+        for (int i = 0; i < 256; ++i) {
+          hipEvent_t x;
+          if (hipEventCreate(&x) != hipSuccess) break;
+          e->ev.push_back(x);
+        }
+      }
+      if (e->ev_used + 2 > e->ev.size()) {
+        on = false;
+        return;
+      }
+      idx = e->ev_used;
+      e->ev_used += 2;
+      (void)hipEventRecord(e->ev[idx], st);
+    }
+  }
+  ~ProbeScope() {
+    if (on) (void)hipEventRecord(e->ev[idx + 1], st);
+  }
+};
+
+// ---------------------------------------------------------------- forward pieces
+struct Ctx {
+  f5h_engine* e;
+  hipStream_t st;
+  Bufs b;
+  int B, N, nt, S, L, nfe, use_cfg, batch_mask;
+};
+
+static GemmArgs gargs(const void* A, int64_t lda, const Lin& W, int M, void* C, int64_t ldc) {
+  GemmArgs g{};
+  g.A = A;
+  g.lda = lda;
+  g.W = W.w;
+  g.ldw = W.K;
+  g.M = M;
+  g.N = W.N;
+  g.K = W.K;
+  g.bias = W.b;
+  g.C = C;
+  g.ldc = ldc;
+  return g;
+}
+
+#define KCK(x)                                                                                  \
+  do {                                                                                          \
+    hipError_t _e = (x);                                                                        \
+    if (_e != hipSuccess) return fail(F5H_EHIP, std::string(#x) + ": " + hipGetErrorString(_e)); \
+  } while (0)
+
+// Everything that depends only on the call's inputs (not on y): time/AdaLN tables, text
+// embedding, hoisted input projection, masks, rope table.
+static int prologue(Ctx& c, const float* t_host, int nt_vals, const float* cond, const uint8_t* cond_mask,
+                    const int64_t* text, const int32_t* duration) {
+  f5h_engine* e = c.e;
+  const f5h_arch& a = e->a;
+  const int d = a.dim, td = a.text_dim, bf = e->bf;
+  Bufs& b = c.b;
+  hipStream_t st = c.st;
+  KCK(rope_table(c.L, b.rope, st));
+  const int off = a.backbone == F5H_DIT ? 0 : 1;
+  if (c.batch_mask) {
+    KCK(build_rowkeep(duration, c.B, c.S, c.L, off, b.rowkeep, st));
+    KCK(build_kvlen(duration, c.B, c.S, off, b.kvlen, st));
+  }
+  // ---- time embedding for every grid point used, then the AdaLN table
+  {
+    KCK(time_sinus(t_host, nt_vals, b.tsin, st));
+    GemmArgs g = gargs(b.tsin, 256, e->t1, nt_vals, b.th, d);
+    KCK(gemm(bf, true, EPI_SILU, g, st));
+    g = gargs(b.th, d, e->t2, nt_vals, b.temb, d);
+    KCK(gemm(bf, true, EPI_STORE, g, st));
+    if (a.backbone == F5H_DIT) {
+      KCK(silu_inplace_copy(b.temb, b.tsilu, (int64_t)nt_vals * d, st));
+      g = gargs(b.tsilu, d, e->ada, nt_vals, b.ada, e->ada.Npad);
+      KCK(gemm(bf, true, EPI_STORE, g, st));
+    }
+  }
+  // ---- text embedding, both branches (cached once per call in the reference, dit.py:294-310)
+  {
+    TextEmbArgs t{};
+    t.text = text;
+    t.B = c.B;
+    t.nt = c.nt;
+    t.N = c.N;
+    t.td = td;
+    t.seq_len = (a.backbone == F5H_DIT && c.batch_mask) ? duration : nullptr;
+    t.table = e->text_table;
+    t.freqs = a.conv_layers > 0 ? e->freqs : nullptr;
+    t.mask_padding = a.text_mask_padding;
+    t.out_c = b.te;
+    t.out_u = b.te + (size_t)c.B * c.N * td;
+    t.keep = b.keepfill;
+    KCK(text_embed(t, st));
+    const int S2 = 2 * c.B, R2 = S2 * c.N;
+    for (int i = 0; i < a.conv_layers; ++i) {
+      CNX& x = e->cnx[i];
+      KCK(dwconv_ln(bf, b.te, S2, c.N, td, x.dw_w, x.dw_b, x.ln_w, x.ln_b, b.dwln, st));
+      GemmArgs g = gargs(b.dwln, td, x.pw1, R2, b.pw1o, 2 * td);
+      KCK(gemm(bf, false, EPI_GELU_ERF, g, st));
+      KCK(grn(bf, b.pw1o, S2, c.N, 2 * td, x.gamma, x.beta, b.grn_scr, b.grno, st));
+      g = gargs(b.grno, 2 * td, x.pw2, R2, b.te, td);
+      g.rowkeep = a.text_mask_padding ? b.keepfill : nullptr;
+      KCK(gemm(bf, false, EPI_RESID_FILL, g, st));
+    }
+  }
+  // ---- hoisted input projection: P = [step_cond | text] . W_ct^T + b
+  KCK(build_ct(bf, cond, cond_mask, b.te, b.te + (size_t)c.B * c.N * td, c.B, c.N, td, c.S, b.act, st));
+  GemmArgs g = gargs(b.act, 128 + e->tdp, e->in_ct, c.S * c.N, b.P, d);
+  KCK(gemm(bf, false, EPI_STORE, g, st));
+  return 0;
+}
+
+// One packed cond/uncond backbone forward at table row k; result in b.p [S, L, mel].
+static int backbone_step(Ctx& c, int k) {
+  f5h_engine* e = c.e;
+  const f5h_arch& a = e->a;
+  const int d = a.dim, bf = e->bf, H = a.heads, inner = H * 64;
+  const bool dit = a.backbone == F5H_DIT;
+  Bufs& b = c.b;
+  hipStream_t st = c.st;
+  const int BN = c.B * c.N;
+  const int rows = c.S * c.L;
+  const uint8_t* keep = c.batch_mask ? b.rowkeep : nullptr;
+  // ---- input embedding: h0 = y.Wx^T + P (both branches), conv position embedding
+  {
+    GemmArgs g = gargs(b.ypad, 128, e->in_x, BN, b.h0, d);
+    g.bias = nullptr;
+    g.add = b.P;
+    g.ld_add = d;
+    g.dual_rows = c.use_cfg ? BN : 0;
+    KCK(gemm(bf, false, EPI_INPROJ, g, st));
+    ConvArgs cv{};
+    cv.S = c.S;
+    cv.L = c.N;
+    cv.d = d;
+    cv.rowkeep = dit ? keep : nullptr;  // UNetT's InputEmbedding passes no mask (unett.py:100)
+    cv.x = b.h0;
+    cv.x_f32 = 1;
+    cv.w = e->conv_w[0];
+    cv.bias = e->conv_b[0];
+    cv.mode = 0;
+    cv.y = b.c1;
+    {
+      ProbeScope ps(e, KC_CONV, st);
+      KCK(conv_pos(bf, cv, st));
+    }
+    cv.x = b.c1;
+    cv.x_f32 = bf ? 0 : 1;
+    cv.w = e->conv_w[1];
+    cv.bias = e->conv_b[1];
+    cv.mode = 1;
+    cv.y = b.h;
+    cv.y_seq_stride = c.L;
+    cv.y_row_off = dit ? 0 : 1;
+    cv.resid = b.h0;
+    KCK(conv_pos(bf, cv, st));
+  }
+  if (!dit) KCK(write_time_token(b.temb + (size_t)k * d, c.S, c.L, d, b.h, st));
+
+  const float* ada_k = dit ? b.ada + (size_t)k * e->ada.Npad : nullptr;
+  float* h = b.h;
+  float* h2 = b.h2;
+  for (int l = 0; l < a.depth; ++l) {
+    Layer& Ly = e->layers[l];
+    const float* ad = ada_k ? ada_k + (size_t)l * 6 * d : nullptr;
+    if (!dit) {
+      if (l < a.depth / 2) {
+        KCK(hipMemcpyAsync(b.skips[l], h, (size_t)rows * d * sizeof(float), hipMemcpyDeviceToDevice, st));
+      } else {
+        GemmArgs g = gargs(h, d, Ly.skip1, rows, h2, d);
+        KCK(gemm(bf, true, EPI_STORE, g, st));
+        g = gargs(b.skips[a.depth - 1 - l], d, Ly.skip2, rows, h2, d);
+        KCK(gemm(bf, true, EPI_RESID, g, st));
+        std::swap(h, h2);
+      }
+      KCK(rms_norm_g(bf, h, rows, d, Ly.g_attn, b.aop, st));
+    } else {
+      KCK(ln_modulate(bf, h, rows, d, ad /*shift_msa*/, ad + d /*scale_msa*/, b.aop, st));
+    }
+    {
+      GemmArgs g = gargs(b.aop, d, Ly.qkv, rows, nullptr, 0);
+      g.rope = b.rope;
+      g.seq_len = c.L;
+      g.heads = H;
+      g.rope_heads = a.pe_attn_head > 0 ? a.pe_attn_head : H;
+      g.q = b.q;
+      g.k = b.k;
+      g.v = b.v;
+      ProbeScope ps(e, KC_QKV, st);
+      KCK(gemm(bf, false, EPI_QKV, g, st));
+    }
+    {
+      AttnArgs at{};
+      at.q = b.q;
+      at.k = b.k;
+      at.v = b.v;
+      at.o = b.o;
+      at.S = c.S;
+      at.H = H;
+      at.L = c.L;
+      at.kv_len = (a.attn_mask_enabled && c.batch_mask) ? b.kvlen : nullptr;
+      at.scale = 0.125f;
+      ProbeScope ps(e, KC_ATTN, st);
+      KCK(attention(bf, at, st));
+    }
+    {
+      GemmArgs g = gargs(b.o, inner, Ly.out, rows, h, d);
+      g.gate = ad ? ad + 2 * d : nullptr;  // gate_msa
+      g.rowkeep = keep;                    // masked_fill of pad rows (modules.py:552-554)
+      KCK(gemm(bf, false, EPI_RESID, g, st));
+    }
+    if (dit)
+      KCK(ln_modulate(bf, h, rows, d, ad + 3 * d /*shift_mlp*/, ad + 4 * d /*scale_mlp*/, b.aop, st));
+    else
+      KCK(rms_norm_g(bf, h, rows, d, Ly.g_ff, b.aop, st));
+    {
+      GemmArgs g = gargs(b.aop, d, Ly.ff1, rows, b.f, a.ff_dim);
+      ProbeScope ps(e, KC_FFN1, st);
+      KCK(gemm(bf, false, EPI_GELU_TANH, g, st));
+    }
+    {
+      GemmArgs g = gargs(b.f, a.ff_dim, Ly.ff2, rows, h, d);
+      g.gate = ad ? ad + 5 * d : nullptr;  // gate_mlp
+      ProbeScope ps(e, KC_FFN2, st);
+      KCK(gemm(bf, false, EPI_RESID, g, st));
+    }
+  }
+  if (dit) {
+    const float* fin = ada_k + (size_t)a.depth * 6 * d;  // AdaLayerNorm_Final: (scale, shift)
+    KCK(ln_modulate(bf, h, rows, d, fin + d, fin, b.aop, st));
+  } else {
+    KCK(rms_norm_g(bf, h, rows, d, e->norm_out_g, b.aop, st));
+  }
+  GemmArgs g = gargs(b.aop, d, e->proj_out, rows, b.p, a.mel_dim);
+  KCK(gemm(bf, false, EPI_STORE, g, st));
+  return 0;
+}
+
+static int check_arch(const f5h_arch* a) {
+  if (!a) return fail(F5H_EINVAL, "null arch");
+  if (a->backbone != F5H_DIT && a->backbone != F5H_UNETT) return fail(F5H_EINVAL, "backbone must be DiT or UNetT");
+  if (a->dim_head != 64) return fail(F5H_EINVAL, "dim_head must be 64");
+  if (a->dim % 128 || a->dim <= 0 || a->dim > 1024) return fail(F5H_EINVAL, "dim must be a multiple of 128, <= 1024");
+  if (a->heads * 64 != a->dim) return fail(F5H_EINVAL, "heads*dim_head must equal dim");
+  if (a->ff_dim % 64 || a->ff_dim <= 0) return fail(F5H_EINVAL, "ff_dim must be a positive multiple of 64");
+  if (a->mel_dim != 100) return fail(F5H_EINVAL, "mel_dim must be 100");
+  if (a->text_dim <= 0 || a->text_dim % 4 || a->text_dim > 512) return fail(F5H_EINVAL, "text_dim must be <= 512, % 4");
+  if (a->depth <= 0 || (a->backbone == F5H_UNETT && a->depth % 2)) return fail(F5H_EINVAL, "bad depth");
+  if (a->backbone == F5H_UNETT && a->conv_layers != 0) return fail(F5H_EINVAL, "UNetT with conv_layers unsupported");
+  if (a->compute != F5H_FP32 && a->compute != F5H_BF16) return fail(F5H_EINVAL, "compute must be FP32 or BF16");
+  return 0;
+}
+
+// ============================================================================ C ABI
+extern "C" {
+
+const char* f5h_last_error(void) { return g_err.c_str(); }
+const char* f5h_version(void) { return "f5h 0.1 gfx950"; }
+
+int f5h_engine_create(const f5h_arch* arch, const f5h_weight* weights, int32_t n_weights, int32_t device,
+                      f5h_engine** out) {
+  if (!out) return fail(F5H_EINVAL, "null out");
+  *out = nullptr;
+  RC(check_arch(arch));
+  HIPCK(hipSetDevice(device));
+  f5h_engine* e = new f5h_engine();
+  e->a = *arch;
+  e->dev = device;
+  e->bf = arch->compute == F5H_BF16;
+  e->esz = e->bf ? 2 : 4;
+  e->tdp = (arch->text_dim + 63) / 64 * 64;
+  WMap W;
+  for (int i = 0; i < n_weights; ++i) W.m[weights[i].name] = {weights[i].data, weights[i].numel};
+  int rc = pack_all(e, W);
+  if (rc) {
+    f5h_engine_destroy(e);
+    return rc;
+  }
+  *out = e;
+  return 0;
+}
+
+void f5h_engine_destroy(f5h_engine* e) {
+  if (!e) return;
+  for (void* p : e->allocs) (void)hipFree(p);
+  for (auto x : e->ev) (void)hipEventDestroy(x);
+  delete e;
+}
+
+size_t f5h_workspace_size(const f5h_engine* e, int32_t B, int32_t N, int32_t nt, int32_t nfe, int32_t use_cfg) {
+  (void)nt;
+  if (!e || B <= 0 || N <= 0 || nfe <= 0) return 0;
+  WS ws;
+  Bufs b;
+  layout(e, ws, b, B, N, nfe + 1, use_cfg);
+  return ws.off;
+}
+
+static int check_ws(f5h_engine* e, int B, int N, int nfe, int use_cfg, void* w, size_t bytes, Ctx& c) {
+  WS ws;
+  layout(e, ws, c.b, B, N, nfe + 1, use_cfg);
+  if (bytes < ws.off)
+    return fail(F5H_ENOMEM, "workspace too small: need " + std::to_string(ws.off) + " have " + std::to_string(bytes));
+  ws.off = 0;
+  ws.base = reinterpret_cast<char*>(w);
+  layout(e, ws, c.b, B, N, nfe + 1, use_cfg);
+  return 0;
+}
+
+int f5h_sample(f5h_engine* e, void* stream, const f5h_sample_args* a, void* workspace, size_t workspace_bytes) {
+  if (!e || !a) return fail(F5H_EINVAL, "null engine/args");
+  if (a->B <= 0 || a->N <= 0 || a->nt < 0 || a->nfe <= 0 || a->nfe > 512)
+    return fail(F5H_EINVAL, "bad B/N/nt/nfe");
+  if (!a->cond || !a->cond_mask || !a->duration || !a->y0 || !a->t_grid || !a->out || (a->nt > 0 && !a->text))
+    return fail(F5H_EINVAL, "null tensor argument");
+  if (e->a.backbone == F5H_DIT && a->N > 8192) return fail(F5H_EINVAL, "N exceeds the text position table (8192)");
+  HIPCK(hipSetDevice(e->dev));
+  Ctx c{};
+  c.e = e;
+  c.st = reinterpret_cast<hipStream_t>(stream);
+  c.B = a->B;
+  c.N = a->N;
+  c.nt = a->nt;
+  c.nfe = a->nfe;
+  c.use_cfg = a->cfg_strength >= 1e-5f;
+  c.S = c.use_cfg ? 2 * c.B : c.B;
+  c.L = e->a.backbone == F5H_DIT ? c.N : c.N + 1;
+  c.batch_mask = a->use_batch_mask ? 1 : 0;
+  RC(check_ws(e, c.B, c.N, c.nfe, c.use_cfg, workspace, workspace_bytes, c));
+  // the ODE evaluates fn at t_0 .. t_{nfe-1}
+  RC(prologue(c, a->t_grid, c.nfe, a->cond, a->cond_mask, a->text, a->duration));
+  const size_t ysz = (size_t)c.B * c.N * e->a.mel_dim;
+  HIPCK(hipMemcpyAsync(a->out, a->y0, ysz * sizeof(float), hipMemcpyDeviceToDevice, c.st));
+  if (a->trajectory)
+    HIPCK(hipMemcpyAsync(a->trajectory, a->y0, ysz * sizeof(float), hipMemcpyDeviceToDevice, c.st));
+  HIPCK(pack_y(e->bf, a->out, c.B * c.N, e->a.mel_dim, c.b.ypad, c.st));
+  for (int k = 0; k < c.nfe; ++k) {
+    RC(backbone_step(c, k));
+    EulerArgs u{};
+    u.y = a->out;
+    u.B = c.B;
+    u.N = c.N;
+    u.mel = e->a.mel_dim;
+    u.p = c.b.p;
+    u.p_seq_stride = (int64_t)c.L * e->a.mel_dim;
+    u.p_row_off = e->a.backbone == F5H_DIT ? 0 : 1;
+    u.p_ld = e->a.mel_dim;
+    u.use_cfg = c.use_cfg;
+    u.cfg = a->cfg_strength;
+    u.dt = a->t_grid[k + 1] - a->t_grid[k];
+    u.ypad = c.b.ypad;
+    u.compute = e->bf;
+    u.traj = a->trajectory ? a->trajectory + (size_t)(k + 1) * ysz : nullptr;
+    HIPCK(cfg_euler(u, c.st));
+  }
+  HIPCK(final_where(a->cond, a->cond_mask, a->out, c.B, c.N, e->a.mel_dim, c.st));
+  return 0;
+}
+
+int f5h_forward(f5h_engine* e, void* stream, const f5h_forward_args* a, void* workspace, size_t workspace_bytes) {
+  if (!e || !a) return fail(F5H_EINVAL, "null engine/args");
+  if (a->B <= 0 || a->N <= 0 || a->nt < 0) return fail(F5H_EINVAL, "bad B/N/nt");
+  if (!a->x || !a->cond || !a->cond_mask || !a->duration || !a->pred || (a->nt > 0 && !a->text))
+    return fail(F5H_EINVAL, "null tensor argument");
+  HIPCK(hipSetDevice(e->dev));
+  Ctx c{};
+  c.e = e;
+  c.st = reinterpret_cast<hipStream_t>(stream);
+  c.B = a->B;
+  c.N = a->N;
+  c.nt = a->nt;
+  c.nfe = 1;
+  c.use_cfg = 1;
+  c.S = 2 * c.B;
+  c.L = e->a.backbone == F5H_DIT ? c.N : c.N + 1;
+  c.batch_mask = a->use_batch_mask ? 1 : 0;
+  RC(check_ws(e, c.B, c.N, 1, 1, workspace, workspace_bytes, c));
+  float tg[2] = {a->t, a->t};
+  RC(prologue(c, tg, 1, a->cond, a->cond_mask, a->text, a->duration));
+  HIPCK(pack_y(e->bf, a->x, c.B * c.N, e->a.mel_dim, c.b.ypad, c.st));
+  RC(backbone_step(c, 0));
+  HIPCK(copy_pred(c.b.p, c.S, c.L, e->a.backbone == F5H_DIT ? 0 : 1, e->a.mel_dim, e->a.mel_dim, a->pred, c.st));
+  return 0;
+}
+
+int f5h_probe_enable(f5h_engine* e, int32_t kclass, int32_t enable) {
+  if (!e) return fail(F5H_EINVAL, "null engine");
+  std::lock_guard<std::mutex> g(e->pm);
+  e->probe_class = enable ? kclass : -1;
+  e->ev_used = 0;
+  e->probe_launches = 0;
+  e->probe_ms = 0.0;
+  return 0;
+}
+
+int f5h_probe_read(f5h_engine* e, int64_t* launches, double* total_ms) {
+  if (!e) return fail(F5H_EINVAL, "null engine");
+  std::lock_guard<std::mutex> g(e->pm);
+  double ms = 0.0;
+  for (size_t i = 0; i + 1 < e->ev_used; i += 2) {
+    HIPCK(hipEventSynchronize(e->ev[i + 1]));
+    float t = 0.f;
+    HIPCK(hipEventElapsedTime(&t, e->ev[i], e->ev[i + 1]));
+    ms += t;
+  }
+  if (launches) *launches = (int64_t)(e->ev_used / 2);
+  if (total_ms) *total_ms = ms;
+  return 0;
+}
+
+// ---------------------------------------------------------------- op-level entry points
+int f5h_op_linear(void* stream, int32_t compute, int32_t M, int32_t N, int32_t K, const float* A, const float* W,
+                  const float* bias, float* C, void* workspace, size_t workspace_bytes) {
+  if (M <= 0 || N <= 0 || K <= 0 || K % 64) return fail(F5H_EINVAL, "op_linear needs K % 64 == 0");
+  const int Npad = (N + 127) / 128 * 128;
+  const size_t es = compute ? 2 : 4;
+  const size_t need = (size_t)Npad * K * es;
+  if (workspace_bytes < need) return fail(F5H_ENOMEM, "workspace too small for op_linear");
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  HIPCK(hipMemsetAsync(workspace, 0, need, st));
+  HIPCK(f32_to_op(compute, W, (int64_t)N * K, workspace, st));
+  GemmArgs g{};
+  g.A = A;
+  g.lda = K;
+  g.W = workspace;
+  g.ldw = K;
+  g.M = M;
+  g.N = N;
+  g.K = K;
+  g.bias = bias;
+  g.C = C;
+  g.ldc = N;
+  HIPCK(gemm(compute, true, EPI_STORE, g, st));
+  return 0;
+}
+
+int f5h_op_attention(void* stream, int32_t compute, int32_t S, int32_t H, int32_t N, const float* Q, const float* K,
+                     const float* V, const int32_t* kv_len, float* O, void* workspace, size_t workspace_bytes) {
+  if (S <= 0 || H <= 0 || N <= 0) return fail(F5H_EINVAL, "bad attention shape");
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  const int64_t n = (int64_t)S * H * N * 64;
+  AttnArgs at{};
+  at.S = S;
+  at.H = H;
+  at.L = N;
+  at.kv_len = kv_len;
+  at.scale = 0.125f;
+  if (compute) {
+    const size_t need = (size_t)n * 2 * 4 + 4 * 256;
+    if (workspace_bytes < need) return fail(F5H_ENOMEM, "workspace too small for op_attention");
+    char* w = reinterpret_cast<char*>(workspace);
+    void *q = w, *k = w + n * 2, *v = w + n * 4, *o = w + n * 6;
+    HIPCK(f32_to_op(1, Q, n, q, st));
+    HIPCK(f32_to_op(1, K, n, k, st));
+    HIPCK(f32_to_op(1, V, n, v, st));
+    at.q = q;
+    at.k = k;
+    at.v = v;
+    at.o = o;
+    HIPCK(attention(1, at, st));
+    HIPCK(op_to_f32(1, o, n, O, st));
+  } else {
+    at.q = Q;
+    at.k = K;
+    at.v = V;
+    at.o = O;
+    HIPCK(attention(0, at, st));
+  }
+  return 0;
+}
+
+}  // extern "C"

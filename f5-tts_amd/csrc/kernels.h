@@ -1,0 +1,115 @@
+// Launcher declarations for the engine's HIP kernels (gfx950).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace f5h {
+
+enum Epi {
+  EPI_STORE = 0,      // C = acc + bias                                  (fp32 out)
+  EPI_SILU = 1,       // C = silu(acc + bias)                            (fp32 out)
+  EPI_GELU_TANH = 2,  // C = gelu_tanh(acc + bias)                       (operand out)
+  EPI_GELU_ERF = 3,   // C = gelu_erf(acc + bias)                        (fp32 out)
+  EPI_RESID = 4,      // C += gate[n] * (acc + bias) * rowkeep[m]        (fp32 in/out)
+  EPI_RESID_FILL = 5, // C = rowkeep[m] ? C + acc + bias : 0             (fp32 in/out)
+  EPI_INPROJ = 6,     // C[m] = acc + add[m]; C[m+dual] = acc + add[m+dual]  (fp32)
+  EPI_QKV = 7,        // RoPE + scatter to q/k/v [S,H,L,64]              (operand out)
+};
+
+struct GemmArgs {
+  const void* A; int64_t lda;      // [M,K] row-major, TA elements
+  const void* W; int64_t ldw;      // [Npad,K] row-major, operand elements (rows padded to 128)
+  int M, N, K;                     // K: multiple of 64 (bf16) / 32 (fp32)
+  const float* bias;               // [N] or null
+  void* C; int64_t ldc;            // output
+  const float* gate;               // EPI_RESID: [N] or null (=1)
+  const uint8_t* rowkeep;          // [M] or null (=1)
+  const float* add; int64_t ld_add;  // EPI_INPROJ addend
+  int64_t dual_rows;               // EPI_INPROJ: second output at row m + dual_rows (0 = none)
+  // EPI_QKV
+  const float2* rope;              // [L][32] (cos, sin)
+  int seq_len;                     // L: rows per sequence
+  int heads, rope_heads;
+  void* q; void* k; void* v;
+};
+
+// compute: 0 fp32 operands, 1 bf16 operands. a_f32: A is fp32 in memory (converted on load).
+hipError_t gemm(int compute, bool a_f32, int epi, const GemmArgs& a, hipStream_t st);
+
+// attention: Q,K,V [S,H,L,64] operand dtype; O [S,L,H*64] operand dtype.
+struct AttnArgs {
+  const void* q; const void* k; const void* v; void* o;
+  int S, H, L;
+  const int32_t* kv_len;  // [S] or null
+  float scale;            // 1/sqrt(64)
+};
+hipError_t attention(int compute, const AttnArgs& a, hipStream_t st);
+
+// grouped conv1d k=31, 16 groups, pad 15 (ConvPositionEmbedding, modules.py:175-201)
+struct ConvArgs {
+  const void* x; int x_f32;        // [S, L, d] input (fp32 or operand dtype)
+  const void* w;                   // packed [16][31][64 out][64 in] operand dtype
+  const float* bias;               // [d]
+  const uint8_t* rowkeep;          // [S*L] or null: input rows masked, output rows masked
+  int S, L, d;
+  // output: mode 0 -> y (operand dtype) = mish(mask(conv)); mode 1 -> y fp32 = mish(mask(conv)) + resid
+  int mode;
+  void* y; int64_t y_seq_stride; int64_t y_row_off;  // in rows
+  const float* resid;              // [S, L, d] fp32 (mode 1)
+};
+hipError_t conv_pos(int compute, const ConvArgs& a, hipStream_t st);
+
+// ---- elementwise / small kernels (elementwise.hip)
+hipError_t time_sinus(const float* t_host, int n, float* out, hipStream_t st);  // host t[n<=512] -> [n,256]
+hipError_t silu_inplace_copy(const float* x, float* y, int64_t n, hipStream_t st);
+// LayerNorm(no affine, eps) * (1 + scale) + shift -> operand dtype; h: [M, d] fp32
+hipError_t ln_modulate(int compute, const float* h, int M, int d, const float* shift, const float* scale,
+                       void* out, hipStream_t st);
+// x_transformers RMSNorm: x / max(||x||, 1e-12) * sqrt(d) * g -> operand dtype
+hipError_t rms_norm_g(int compute, const float* h, int M, int d, const float* g, void* out, hipStream_t st);
+hipError_t rope_table(int L, float2* out, hipStream_t st);
+// text tokens -> embeddings (dit.py:86-120 / unett.py:53-64), both branches
+struct TextEmbArgs {
+  const int64_t* text; int B, nt, N, td;
+  const int32_t* seq_len;       // [B] per-sample valid length or null (= N for all)
+  const float* table;           // [V, td]
+  const float* freqs;           // [8192, td] or null (no sinus pos)
+  int mask_padding;
+  float* out_c; float* out_u;   // [B, N, td] each
+  uint8_t* keep;                // [2B*N] !fill (for masked_fill after each block) or null
+};
+hipError_t text_embed(const TextEmbArgs& a, hipStream_t st);
+// depthwise conv k7 pad3 + bias then LayerNorm(affine, eps 1e-6) -> operand dtype. x: [S, L, C] fp32
+hipError_t dwconv_ln(int compute, const float* x, int S, int L, int C, const float* dw_w, const float* dw_b,
+                     const float* ln_w, const float* ln_b, void* out, hipStream_t st);
+// GRN: sumsq[s,c] = sum_n x^2 ; then out = gamma*(x*Nx)+beta+x -> operand dtype
+hipError_t grn(int compute, const float* x, int S, int L, int C, const float* gamma, const float* beta,
+               float* scratch /*[S*C + S]*/, void* out, hipStream_t st);
+// A_ct [S*N, 128 + td] operand dtype: [where(cond_mask,cond,0) (zeros for uncond) pad 128 | text]
+hipError_t build_ct(int compute, const float* cond, const uint8_t* cond_mask, const float* text_c,
+                    const float* text_u, int B, int N, int td, int S, void* out, hipStream_t st);
+// y (fp32 [B,N,mel]) -> ypad operand [B*N, 128]
+hipError_t pack_y(int compute, const float* y, int rows, int mel, void* ypad, hipStream_t st);
+// CFG + Euler: y += dt * (pc + (pc - pu) * cfg); pred rows from p with row offset/stride.
+struct EulerArgs {
+  float* y; int B, N, mel;
+  const float* p; int64_t p_seq_stride; int p_row_off; int64_t p_ld;  // p[s, row_off + n, c]
+  int use_cfg; float cfg; float dt;
+  void* ypad; int compute;      // refreshed operand copy (or null)
+  float* traj;                  // [B,N,mel] slot to copy y into (or null)
+};
+hipError_t cfg_euler(const EulerArgs& a, hipStream_t st);
+hipError_t final_where(const float* cond, const uint8_t* cond_mask, float* y, int B, int N, int mel,
+                       hipStream_t st);
+// rowkeep[s*L + pos] = (pos - off < dur[s % B]) || pos < off ; for S sequences
+hipError_t build_rowkeep(const int32_t* dur, int B, int S, int L, int off, uint8_t* keep, hipStream_t st);
+// kv_len[s] = dur[s % B] + off
+hipError_t build_kvlen(const int32_t* dur, int B, int S, int off, int32_t* kv, hipStream_t st);
+// h[s, 0, :] = temb (UNetT time token)
+hipError_t write_time_token(const float* temb, int S, int L, int d, float* h, hipStream_t st);
+// extract rows [s, 1..L-1] of pred -> dst [S, L-1, mel]
+hipError_t copy_pred(const float* p, int S, int L, int row_off, int mel, int64_t p_ld, float* dst, hipStream_t st);
+hipError_t f32_to_op(int compute, const float* x, int64_t n, void* out, hipStream_t st);
+hipError_t op_to_f32(int compute, const void* x, int64_t n, float* out, hipStream_t st);
+
+}  // namespace f5h

@@ -1,0 +1,182 @@
+"""Python handle on the HIP engine (libf5h.so). Plumbing only: device memory and the
+current stream come from PyTorch; every FLOP runs in the engine's kernels."""
+
+from __future__ import annotations
+
+import ctypes
+import threading
+
+import numpy as np
+import torch
+
+from . import _lib
+
+
+def _arch_struct(arch: dict, compute: str) -> _lib.Arch:
+    a = _lib.Arch()
+    a.backbone = _lib.F5H_DIT if arch["backbone"] == "DiT" else _lib.F5H_UNETT
+    a.dim = arch["dim"]
+    a.depth = arch["depth"]
+    a.heads = arch["heads"]
+    a.dim_head = arch.get("dim_head", 64)
+    a.ff_dim = int(arch["dim"] * arch["ff_mult"])
+    a.text_dim = arch["text_dim"] if arch.get("text_dim") is not None else arch["mel_dim"]
+    a.text_num_embeds = arch["text_num_embeds"]
+    a.mel_dim = arch["mel_dim"]
+    a.conv_layers = arch.get("conv_layers", 0)
+    a.text_mask_padding = int(bool(arch.get("text_mask_padding", True)))
+    a.pe_attn_head = int(arch.get("pe_attn_head") or 0)
+    a.attn_mask_enabled = int(bool(arch.get("attn_mask_enabled", False)))
+    a.compute = {"fp32": _lib.F5H_FP32, "bf16": _lib.F5H_BF16}[compute]
+    if arch.get("qk_norm"):
+        raise NotImplementedError("qk_norm is not used by any shipped config (F5TTS_*.yaml qk_norm: null)")
+    if arch.get("long_skip_connection") or arch.get("text_embedding_average_upsampling"):
+        raise NotImplementedError("long_skip_connection / average upsampling are off in every shipped config")
+    return a
+
+
+class Engine:
+    """One packed model on one device. Immutable after construction, so one instance may
+    serve concurrent `sample` calls from several host threads (each call allocates its own
+    workspace from the torch caching allocator)."""
+
+    def __init__(self, arch: dict, weights: dict, compute: str = "bf16", device=None):
+        L = _lib.lib()
+        self.arch = dict(arch)
+        self.compute = compute
+        self.device = torch.device("cuda", torch.cuda.current_device() if device is None else
+                                   torch.device(device).index or 0)
+        host = {}
+        for k, v in weights.items():
+            k = k[len("transformer."):] if k.startswith("transformer.") else k
+            if isinstance(v, torch.Tensor):
+                v = v.detach().to("cpu", torch.float32).contiguous().numpy()
+            host[k] = np.ascontiguousarray(v, dtype=np.float32)
+        names = [k.encode() for k in host]
+        arr = (_lib.Weight * len(host))()
+        for i, (k, v) in enumerate(host.items()):
+            arr[i].name = names[i]
+            arr[i].data = v.ctypes.data
+            arr[i].numel = v.size
+        a = _arch_struct(self.arch, compute)
+        h = ctypes.c_void_p()
+        with torch.cuda.device(self.device):
+            _lib.check(L.f5h_engine_create(ctypes.byref(a), arr, len(host), self.device.index, ctypes.byref(h)),
+                       "f5h_engine_create")
+        self._h = h
+        self._lock = threading.Lock()
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h is not None and h.value:
+            try:
+                _lib.lib().f5h_engine_destroy(h)
+            except Exception:
+                pass
+            self._h = None
+
+    # ------------------------------------------------------------------ workspace
+    def workspace_bytes(self, B, N, nt, nfe, use_cfg=True) -> int:
+        return int(_lib.lib().f5h_workspace_size(self._h, B, N, nt, nfe, int(use_cfg)))
+
+    def _workspace(self, nbytes):
+        return torch.empty(max(nbytes, 256), dtype=torch.uint8, device=self.device)
+
+    # ------------------------------------------------------------------ calls
+    def sample(self, cond, cond_mask, text, duration, y0, t_grid, cfg_strength, use_batch_mask,
+               out=None, keep_trajectory=True, workspace=None):
+        """Run the CFM ODE loop. Tensors on this engine's device:
+        cond f32 [B,N,mel], cond_mask bool/u8 [B,N], text int64 [B,nt], duration int [B],
+        y0 f32 [B,N,mel]; t_grid: host sequence of nfe+1 floats."""
+        B, N, mel = cond.shape
+        nt = text.shape[1]
+        tg = np.ascontiguousarray(np.asarray(t_grid, dtype=np.float32))
+        nfe = tg.shape[0] - 1
+        cond = cond.to(self.device, torch.float32).contiguous()
+        cmask = cond_mask.to(self.device, torch.uint8).contiguous()
+        text = text.to(self.device, torch.int64).contiguous()
+        dur = duration.to(self.device, torch.int32).contiguous()
+        y0 = y0.to(self.device, torch.float32).contiguous()
+        if out is None:
+            out = torch.empty(B, N, mel, dtype=torch.float32, device=self.device)
+        traj = (torch.empty(nfe + 1, B, N, mel, dtype=torch.float32, device=self.device)
+                if keep_trajectory else None)
+        use_cfg = cfg_strength >= 1e-5
+        need = self.workspace_bytes(B, N, nt, nfe, use_cfg)
+        ws = workspace if workspace is not None and workspace.numel() >= need else self._workspace(need)
+        a = _lib.SampleArgs()
+        a.B, a.N, a.nt, a.nfe = B, N, nt, nfe
+        a.cond, a.cond_mask, a.text, a.duration, a.y0 = (cond.data_ptr(), cmask.data_ptr(), text.data_ptr(),
+                                                         dur.data_ptr(), y0.data_ptr())
+        a.t_grid = tg.ctypes.data
+        a.cfg_strength = float(cfg_strength)
+        a.use_batch_mask = int(bool(use_batch_mask))
+        a.out = out.data_ptr()
+        a.trajectory = traj.data_ptr() if traj is not None else None
+        with torch.cuda.device(self.device):
+            _lib.check(_lib.lib().f5h_sample(self._h, _lib.stream_handle(self.device), ctypes.byref(a),
+                                             ws.data_ptr(), ws.numel()), "f5h_sample")
+        return out, traj
+
+    def forward(self, x, cond, cond_mask, text, duration, t: float, use_batch_mask):
+        """One packed cond/uncond backbone forward -> pred [2B,N,mel] (DiT.forward(cfg_infer=True))."""
+        B, N, mel = x.shape
+        nt = text.shape[1]
+        x = x.to(self.device, torch.float32).contiguous()
+        cond = cond.to(self.device, torch.float32).contiguous()
+        cmask = cond_mask.to(self.device, torch.uint8).contiguous()
+        text = text.to(self.device, torch.int64).contiguous()
+        dur = duration.to(self.device, torch.int32).contiguous()
+        pred = torch.empty(2 * B, N, mel, dtype=torch.float32, device=self.device)
+        ws = self._workspace(self.workspace_bytes(B, N, nt, 1, True))
+        a = _lib.ForwardArgs()
+        a.B, a.N, a.nt = B, N, nt
+        a.x, a.cond, a.cond_mask, a.text, a.duration = (x.data_ptr(), cond.data_ptr(), cmask.data_ptr(),
+                                                        text.data_ptr(), dur.data_ptr())
+        a.t = float(t)
+        a.use_batch_mask = int(bool(use_batch_mask))
+        a.pred = pred.data_ptr()
+        with torch.cuda.device(self.device):
+            _lib.check(_lib.lib().f5h_forward(self._h, _lib.stream_handle(self.device), ctypes.byref(a),
+                                              ws.data_ptr(), ws.numel()), "f5h_forward")
+        return pred
+
+    # ------------------------------------------------------------------ kernel probe
+    def probe(self, kclass: str | None):
+        L = _lib.lib()
+        if kclass is None:
+            _lib.check(L.f5h_probe_enable(self._h, 0, 0), "probe")
+        else:
+            _lib.check(L.f5h_probe_enable(self._h, _lib.KCLASS[kclass], 1), "probe")
+
+    def probe_read(self):
+        n = ctypes.c_int64()
+        ms = ctypes.c_double()
+        _lib.check(_lib.lib().f5h_probe_read(self._h, ctypes.byref(n), ctypes.byref(ms)), "probe_read")
+        return n.value, ms.value
+
+
+# ---------------------------------------------------------------- op-level helpers (tests)
+def op_linear(A, W, bias=None, compute="bf16"):
+    M, K = A.shape
+    N = W.shape[0]
+    C = torch.empty(M, N, dtype=torch.float32, device=A.device)
+    ws = torch.empty(((N + 127) // 128 * 128) * K * 4 + 256, dtype=torch.uint8, device=A.device)
+    c = {"fp32": 0, "bf16": 1}[compute]
+    _lib.check(_lib.lib().f5h_op_linear(_lib.stream_handle(A.device), c, M, N, K, A.contiguous().data_ptr(),
+                                        W.contiguous().data_ptr(), _lib.ptr(bias), C.data_ptr(), ws.data_ptr(),
+                                        ws.numel()), "f5h_op_linear")
+    return C
+
+
+def op_attention(Q, K, V, kv_len=None, compute="bf16"):
+    S, H, N, D = Q.shape
+    assert D == 64
+    O = torch.empty(S, N, H * 64, dtype=torch.float32, device=Q.device)
+    ws = torch.empty(Q.numel() * 8 + 1024, dtype=torch.uint8, device=Q.device)
+    c = {"fp32": 0, "bf16": 1}[compute]
+    kv = None if kv_len is None else kv_len.to(Q.device, torch.int32).contiguous()
+    _lib.check(_lib.lib().f5h_op_attention(_lib.stream_handle(Q.device), c, S, H, N, Q.contiguous().data_ptr(),
+                                           K.contiguous().data_ptr(), V.contiguous().data_ptr(), _lib.ptr(kv),
+                                           O.data_ptr(), ws.data_ptr(), ws.numel()), "f5h_op_attention")
+    return O

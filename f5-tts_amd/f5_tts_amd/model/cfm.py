@@ -1,0 +1,121 @@
+"""Engine-backed conditional flow matching sampler: a drop-in `model_obj` for
+`infer_process` / `F5TTS.ema_model` / eval drivers.
+
+`CFM.sample` keeps the reference signature and return tuple (`cfm.py:83-102,229`). The host
+preamble (mel intake, tokenisation, duration rule, cond padding/masks, noise recipe, time
+grid) is restated here in PyTorch exactly as `cfm.py:105-216` does it; the ODE loop, the
+backbone forwards, CFG, the Euler update and the final cond overwrite run in the HIP
+engine (`f5h_sample`, include/f5h.h). There is no PyTorch fallback for the loop.
+"""
+
+from __future__ import annotations
+
+from typing import Callable
+
+import torch
+import torch.nn.functional as F
+from torch import nn
+from torch.nn.utils.rnn import pad_sequence
+
+from .utils import default, exists, lens_to_mask, list_str_to_idx, list_str_to_tensor, time_grid
+
+
+class CFM(nn.Module):
+    def __init__(self, transformer: nn.Module, sigma=0.0, odeint_kwargs: dict = dict(method="euler"),
+                 audio_drop_prob=0.3, cond_drop_prob=0.2, num_channels=None, mel_spec_module: nn.Module | None = None,
+                 mel_spec_kwargs: dict = dict(), frac_lengths_mask=(0.7, 1.0), vocab_char_map: dict | None = None,
+                 compute: str = "auto"):
+        super().__init__()
+        if odeint_kwargs.get("method", "euler") != "euler":
+            raise NotImplementedError("the engine integrates with fixed-grid Euler (the reference default, "
+                                      "utils_infer.py:62 ode_method='euler')")
+        self.frac_lengths_mask = frac_lengths_mask
+        if mel_spec_module is None:
+            from ..mel import MelSpec
+
+            mel_spec_module = MelSpec(**mel_spec_kwargs)
+        self.mel_spec = mel_spec_module
+        self.num_channels = default(num_channels, getattr(self.mel_spec, "n_mel_channels", 100))
+        self.audio_drop_prob = audio_drop_prob
+        self.cond_drop_prob = cond_drop_prob
+        self.transformer = transformer
+        self.dim = transformer.dim
+        self.sigma = sigma
+        self.odeint_kwargs = odeint_kwargs
+        self.vocab_char_map = vocab_char_map
+        self.compute = compute  # "auto" | "bf16" | "fp32"
+
+    @property
+    def device(self):
+        return next(self.parameters()).device
+
+    def engine_compute(self) -> str:
+        if self.compute != "auto":
+            return self.compute
+        return "fp32" if next(self.parameters()).dtype == torch.float32 else "bf16"
+
+    @torch.no_grad()
+    def sample(self, cond, text, duration, *, lens=None, steps=32, cfg_strength=1.0, sway_sampling_coef=None,
+               seed: int | None = None, max_duration=65536, vocoder: Callable | None = None, use_epss=True,
+               no_ref_audio=False, duplicate_test=False, t_inter=0.1, edit_mask=None, y0=None,
+               keep_trajectory: bool = True):
+        """Same arguments/returns as the reference `CFM.sample`; extra keyword `y0` supplies the
+        initial noise explicitly (parity tests), `keep_trajectory=False` skips the [steps+1,...] copy."""
+        self.eval()
+        if duplicate_test:
+            raise NotImplementedError("duplicate_test is a debugging corner of the reference (cfm.py:141-143)")
+        pdtype = next(self.parameters()).dtype
+        if cond.ndim == 2:  # raw wave -> mel (cfm.py:106-109)
+            cond = self.mel_spec(cond)
+            cond = cond.permute(0, 2, 1)
+            assert cond.shape[-1] == self.num_channels
+        cond = cond.to(pdtype)
+        batch, cond_seq_len, device = *cond.shape[:2], cond.device
+        if not exists(lens):
+            lens = torch.full((batch,), cond_seq_len, device=device, dtype=torch.long)
+
+        if isinstance(text, list):
+            if exists(self.vocab_char_map):
+                text = list_str_to_idx(text, self.vocab_char_map).to(device)
+            else:
+                text = list_str_to_tensor(text).to(device)
+            assert text.shape[0] == batch
+
+        cond_mask = lens_to_mask(lens)
+        if edit_mask is not None:
+            cond_mask = cond_mask & edit_mask
+        if isinstance(duration, int):
+            duration = torch.full((batch,), duration, device=device, dtype=torch.long)
+        duration = torch.maximum(torch.maximum((text != -1).sum(dim=-1), lens) + 1, duration)
+        duration = duration.clamp(max=max_duration)
+        max_duration = int(duration.amax())
+
+        cond = F.pad(cond, (0, 0, 0, max_duration - cond_seq_len), value=0.0)
+        if no_ref_audio:
+            cond = torch.zeros_like(cond)
+        cond_mask = F.pad(cond_mask, (0, max_duration - cond_mask.shape[-1]), value=False)
+        use_batch_mask = batch > 1  # cfm.py:155-158
+
+        if y0 is None:  # noise recipe of cfm.py:196-201 (per utterance, same seed each)
+            ys = []
+            for dur in duration:
+                if exists(seed):
+                    torch.manual_seed(seed)
+                ys.append(torch.randn(int(dur), self.num_channels, device=self.device, dtype=pdtype))
+            y0 = pad_sequence(ys, padding_value=0, batch_first=True)
+
+        t = time_grid(steps, sway_sampling_coef, use_epss, device=self.device, dtype=pdtype)
+        t_host = t.float().cpu().numpy()
+
+        eng = self.transformer.get_engine(self.engine_compute(), self.device)
+        out, traj = eng.sample(cond.float(), cond_mask, text, duration, y0.float(), t_host, float(cfg_strength),
+                               use_batch_mask, keep_trajectory=keep_trajectory)
+        out = out.to(pdtype)
+        if traj is not None:
+            traj = traj.to(pdtype)
+        if exists(vocoder):
+            out = vocoder(out.permute(0, 2, 1))
+        return out, traj
+
+    def forward(self, *args, **kwargs):
+        raise NotImplementedError("training (CFM.forward, cfm.py:231-302) is out of scope for the sampling engine")

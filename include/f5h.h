@@ -1,0 +1,145 @@
+/*
+ * f5h.h — C ABI of the MI355X (gfx950) CFM sampling engine.
+ *
+ * The engine replaces the hot path of the reference:
+ *   CFM.sample()            /root/reference/src/f5_tts/model/cfm.py:83-229   (Euler ODE + CFG loop)
+ *   DiT.forward()           /root/reference/src/f5_tts/model/backbones/dit.py:319-370
+ *   UNetT.forward()         /root/reference/src/f5_tts/model/backbones/unett.py:244-307
+ * behind the reference's own Python surface (`model_obj.sample(...)`, called from
+ * infer/utils_infer.py:497-504, eval/eval_infer_batch.py:190-200, runtime/.../benchmark.py:415-423).
+ *
+ * Plain C types only: pointers, sizes, ints. No torch types cross this boundary.
+ * Every entry point returns 0 on success, a negative f5h_status otherwise; the
+ * message is available from f5h_last_error() (thread-local).
+ *
+ * Ownership: the engine owns its packed device weights and is immutable after
+ * f5h_engine_create (shareable between host threads). The caller owns every I/O
+ * buffer and the workspace, so concurrent calls on different workspaces are
+ * re-entrant (this replaces the reference's thread-local text cache, dit.py:237-262).
+ * All work is enqueued on the caller's hipStream_t (passed as void*).
+ */
+#ifndef F5H_H
+#define F5H_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum f5h_status {
+  F5H_OK = 0,
+  F5H_EINVAL = -1,   /* bad argument / shape */
+  F5H_EHIP = -2,     /* HIP runtime error */
+  F5H_ENOWEIGHT = -3,/* missing or mis-shaped weight */
+  F5H_ENOMEM = -4,   /* workspace too small */
+};
+
+enum f5h_backbone { F5H_DIT = 0, F5H_UNETT = 1 };
+enum f5h_compute { F5H_FP32 = 0, F5H_BF16 = 1 };
+
+/* Architecture: mirrors DiT.__init__ (dit.py:171-192) / UNetT.__init__ (unett.py:108-129)
+ * and the Hydra arch block (configs/F5TTS_v1_Base.yaml:24-37). */
+typedef struct f5h_arch {
+  int32_t backbone;          /* f5h_backbone */
+  int32_t dim;               /* model width d (multiple of 64) */
+  int32_t depth;             /* blocks */
+  int32_t heads;             /* attention heads */
+  int32_t dim_head;          /* must be 64 */
+  int32_t ff_dim;            /* int(dim * ff_mult) */
+  int32_t text_dim;          /* text embedding width (DiT: 512; UNetT: mel_dim) */
+  int32_t text_num_embeds;   /* vocab size (embedding has text_num_embeds+1 rows) */
+  int32_t mel_dim;           /* 100 */
+  int32_t conv_layers;       /* ConvNeXtV2 text blocks */
+  int32_t text_mask_padding; /* 0/1 */
+  int32_t pe_attn_head;      /* 0 = rope on all heads, k>0 = first k heads (modules.py:503-506) */
+  int32_t attn_mask_enabled; /* 0/1: key-padding mask in attention (modules.py:512-516) */
+  int32_t compute;           /* f5h_compute: FP32 parity mode or BF16 MFMA mode */
+} f5h_arch;
+
+/* One named parameter, host memory, float32, C-contiguous, with the reference's
+ * state-dict name minus the `transformer.` prefix (e.g. "transformer_blocks.3.attn.to_q.weight"). */
+typedef struct f5h_weight {
+  const char* name;
+  const float* data;
+  int64_t numel;
+} f5h_weight;
+
+typedef struct f5h_engine f5h_engine;
+
+/* Replaces: model construction + load_checkpoint (utils_infer.py:190-276): packs the
+ * weights into the engine's device layout (bf16 or fp32 GEMM panels, conv taps, the
+ * concatenated AdaLN matrix). Blocks until the upload is complete. */
+int f5h_engine_create(const f5h_arch* arch, const f5h_weight* weights, int32_t n_weights,
+                      int32_t device, f5h_engine** out);
+void f5h_engine_destroy(f5h_engine* eng);
+
+/* Arguments of one CFM.sample call after the host preamble of cfm.py:105-158 and
+ * the noise/time-grid recipe of cfm.py:196-216. All pointers are DEVICE pointers
+ * except t_grid (host). Shapes: B utterances, N = max duration (padded frames),
+ * nt text tokens. */
+typedef struct f5h_sample_args {
+  int32_t B, N, nt, nfe;
+  const float* cond;         /* [B,N,mel] padded cond mel (cfm.py:148) */
+  const uint8_t* cond_mask;  /* [B,N] 1 = keep cond (lens_to_mask(lens) & edit_mask, cfm.py:128-130) */
+  const int64_t* text;       /* [B,nt] token ids, -1 = pad (utils.py:99-106) */
+  const int32_t* duration;   /* [B] per-utterance total frames (cfm.py:135-139) */
+  const float* y0;           /* [B,N,mel] initial noise, zero-padded (cfm.py:196-201) */
+  const float* t_grid;       /* HOST [nfe+1] time grid, EPSS/linspace + sway (cfm.py:211-216) */
+  float cfg_strength;        /* < 1e-5 disables the packed uncond branch (cfm.py:167) */
+  int32_t use_batch_mask;    /* 1 when B>1 (cfm.py:155-158) */
+  float* out;                /* [B,N,mel] result: where(cond_mask, cond, y_final) (cfm.py:223) */
+  float* trajectory;         /* [nfe+1,B,N,mel] or NULL (odeint output, cfm.py:218) */
+} f5h_sample_args;
+
+/* Bytes of workspace f5h_sample needs for a call of this shape. */
+size_t f5h_workspace_size(const f5h_engine* eng, int32_t B, int32_t N, int32_t nt, int32_t nfe,
+                          int32_t use_cfg);
+
+/* Replaces CFM.sample's ODE loop (cfm.py:160-223): text embedding once, then nfe Euler
+ * steps each running one packed cond/uncond backbone forward, CFG combine and the update,
+ * then the final cond overwrite. Everything enqueued on `stream` (a hipStream_t). */
+int f5h_sample(f5h_engine* eng, void* stream, const f5h_sample_args* args, void* workspace,
+               size_t workspace_bytes);
+
+/* One packed backbone forward (DiT.forward / UNetT.forward with cfg_infer=True, cache=True):
+ * x [B,N,mel], step_cond = where(cond_mask,cond,0) computed from cond/cond_mask, time t.
+ * Writes pred [2B,N,mel] (cond rows then uncond rows). Used for op-level parity. */
+typedef struct f5h_forward_args {
+  int32_t B, N, nt;
+  const float* x;
+  const float* cond;
+  const uint8_t* cond_mask;
+  const int64_t* text;
+  const int32_t* duration;
+  float t;
+  int32_t use_batch_mask;
+  float* pred;               /* [2B,N,mel] */
+} f5h_forward_args;
+int f5h_forward(f5h_engine* eng, void* stream, const f5h_forward_args* args, void* workspace,
+                size_t workspace_bytes);
+
+/* Kernel probe: when enabled the engine brackets every launch of kernel class `kclass`
+ * with HIP events on the launch stream; f5h_probe_read returns (launches, total ms).
+ * Classes: 0 = FFN1 GEMM, 1 = attention, 2 = QKV GEMM, 3 = FFN2 GEMM, 4 = conv. */
+int f5h_probe_enable(f5h_engine* eng, int32_t kclass, int32_t enable);
+int f5h_probe_read(f5h_engine* eng, int64_t* launches, double* total_ms);
+
+/* Op-level entry points (parity tests / microbenchmarks). Device pointers, row-major. */
+/* C[M,N] = A[M,K] . W[N,K]^T + bias  (fp32 in/out; compute = F5H_FP32 or F5H_BF16 operands) */
+int f5h_op_linear(void* stream, int32_t compute, int32_t M, int32_t N, int32_t K, const float* A,
+                  const float* W, const float* bias, float* C, void* workspace, size_t workspace_bytes);
+/* O[S,N,H*64] = softmax(Q K^T / 8 [+key mask]) V with Q,K,V [S,H,N,64] fp32;
+ * kv_len: [S] valid keys per sequence or NULL. */
+int f5h_op_attention(void* stream, int32_t compute, int32_t S, int32_t H, int32_t N, const float* Q,
+                     const float* K, const float* V, const int32_t* kv_len, float* O, void* workspace,
+                     size_t workspace_bytes);
+
+const char* f5h_last_error(void);
+const char* f5h_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* F5H_H */
