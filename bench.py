@@ -1,0 +1,196 @@
+"""Benchmark: F5-TTS Base (v1) CFM.sample on MI355X through the HIP engine.
+
+Workload (BASELINE.json configs[1] = SURVEY C2): F5TTS_v1_Base, bf16 MFMA engine, NFE 16
+(EPSS grid) + sway -1, CFG 2.0, B=1 per GPU, 10 s prompt (938 ref frames) + 938 generated
+frames = 1876 frames, 300 text tokens. One "step" = one full `CFM.sample()` call (text
+embedding, 16 packed cond/uncond DiT forwards, CFG + Euler, final cond overwrite) plus the
+RCCL all-gather of the finished mels. Synthetic data and hash-PRNG weights of the real
+architecture (checkpoints are network-only).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    torchrun --nproc-per-node N bench.py --gpus N ...   (one rank per GPU, weak scaling)
+
+Prints ONE JSON line on rank 0 (contract in the task statement).
+"""
+
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+for _p in (REPO, os.path.join(REPO, "f5-tts_amd")):
+    if _p not in sys.path:
+        sys.path.insert(0, _p)
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+HOP, SR = 256, 24000
+PEAK_BF16_TFLOPS = 2500.0  # MI355X dense bf16 MFMA (MI355X_MICROARCH.md chip table)
+
+
+def attn_flops(S, H, L):
+    return 4.0 * S * H * L * L * 64  # QK^T + PV per launch
+
+
+def build_model(preset, compute, device):
+    from f5_tts_amd import configs, synthetic
+    from f5_tts_amd.model import CFM, DiT, UNetT
+
+    arch = configs.get_arch(preset)
+    cls = DiT if arch["backbone"] == "DiT" else UNetT
+    kw = {k: v for k, v in arch.items() if k not in ("backbone", "text_num_embeds", "mel_dim")}
+    net = cls(**kw, text_num_embeds=arch["text_num_embeds"], mel_dim=arch["mel_dim"])
+    net.load_state_dict(synthetic.make_weights_torch(arch), strict=False)
+    return CFM(transformer=net, num_channels=100, compute=compute).to(device), arch
+
+
+def cpu_baseline(case, arch, threads):
+    """Oracle (fp32 PyTorch-CPU restatement) on a bounded sample of the same workload:
+    1 and 3 Euler steps of the C2 call; full-call time extrapolated as prologue + NFE x step."""
+    from f5_tts_amd import synthetic
+    from oracle import ref_cpu
+
+    torch.set_num_threads(threads)
+    W = synthetic.make_weights_torch(arch)
+    inp = synthetic.make_case(B=1, ref_frames=case["ref"], total_frames=case["total"], n_text=case["nt"])
+    t = {}
+    for ms in (1, 3):
+        t0 = time.perf_counter()
+        ref_cpu.cfm_sample(W, arch, inp["cond"], inp["text"], inp["duration"], lens=inp["lens"], steps=case["nfe"],
+                           cfg_strength=case["cfg"], sway_sampling_coef=case["sway"], seed=0, max_steps=ms)
+        t[ms] = time.perf_counter() - t0
+    step = (t[3] - t[1]) / 2
+    full = (t[1] - step) + case["nfe"] * step
+    gen = case["total"] - case["ref"]
+    return {"value": gen / full, "unit": "mel-frames/s", "cores": torch.get_num_threads(), "kind": "port",
+            "sample": f"oracle/ref_cpu.py fp32, C2 call truncated to 1 and 3 Euler steps "
+                      f"({t[1]:.1f}s, {t[3]:.1f}s); full 16-step call extrapolated = {full:.1f}s",
+            "rtf": full / (gen * HOP / SR)}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--preset", default="F5TTS_v1_Base")
+    ap.add_argument("--compute", default="bf16")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--probe", default="attention", help="kernel class timed with HIP events for the roofline")
+    args = ap.parse_args()
+
+    from f5_tts_amd import synthetic
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    device = torch.device("cuda", local)
+    torch.cuda.set_device(device)
+
+    case = synthetic.c2_case()
+    case["preset"] = args.preset
+    model, arch = build_model(args.preset, args.compute, device)
+    inp = synthetic.make_case(B=1, ref_frames=case["ref"], total_frames=case["total"], n_text=case["nt"],
+                              seed=1234 + rank)
+    cond, text = inp["cond"].to(device), inp["text"].to(device)
+    duration, lens = inp["duration"].to(device), inp["lens"].to(device)
+    gen_frames = case["total"] - case["ref"]
+    gathered = torch.empty(world, gen_frames, 100, device=device)
+
+    def step():
+        out, _ = model.sample(cond=cond, text=text, duration=duration, lens=lens, steps=case["nfe"],
+                              cfg_strength=case["cfg"], sway_sampling_coef=case["sway"], seed=rank)
+        mel = out[0, case["ref"]:].contiguous()
+        if world > 1:
+            dist.all_gather_into_tensor(gathered, mel)  # finished mels only
+        return mel
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+
+    eng = model.transformer.get_engine(model.engine_compute(), device)
+    eng.probe(args.probe)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    n_launch, probe_ms = eng.probe_read()
+    eng.probe(None)
+    if world > 1:
+        tt = torch.tensor([elapsed], device=device, dtype=torch.float64)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt.item())
+
+    frames = gen_frames * args.steps * world
+    value = frames / elapsed
+    ms_per_step = elapsed / args.steps * 1e3
+    rtf = elapsed / (frames * HOP / SR) * world  # wall / generated audio seconds, per GPU stream
+
+    S, H, L = 2, arch["heads"], case["total"]
+    roof = None
+    if n_launch:
+        avg_ms = probe_ms / n_launch
+        if args.probe == "attention":
+            fl = attn_flops(S, H, L)
+        elif args.probe in ("ffn1", "ffn2"):
+            fl = 2.0 * S * L * arch["dim"] * int(arch["dim"] * arch["ff_mult"])
+        elif args.probe == "qkv":
+            fl = 2.0 * S * L * arch["dim"] * 3 * arch["dim"]
+        else:
+            fl = 2.0 * S * L * arch["dim"] * (arch["dim"] // 16) * 31
+        ach = fl / (avg_ms * 1e-3) / 1e12
+        roof = {"bound": "mfma", "kernel": args.probe, "achieved": round(ach, 2), "peak": PEAK_BF16_TFLOPS,
+                "unit": "TFLOP/s", "frac": round(ach / PEAK_BF16_TFLOPS, 4), "traffic": None,
+                "avg_launch_ms": round(avg_ms, 5), "launches": n_launch, "flops_per_launch": fl}
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(case, arch, threads=min(16, os.cpu_count() or 1))
+
+    # whole-path algorithmic FLOPs: NFE * S * F(N), F(N) = 378.888e6 N + 90112 N^2 (Base)
+    flops_call = case["nfe"] * S * (378.888e6 * L + 90112.0 * L * L)
+    if rank == 0:
+        line = {
+            "metric": "mel-frames/s (RTF alongside), F5-TTS Base NFE=16 CFM.sample",
+            "value": round(value, 2),
+            "unit": "mel-frames/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms_per_step, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": args.compute,
+            "data": "synthetic (hash-PRNG weights of F5TTS_v1_Base, N(-4,2) cond mel, uniform text ids)",
+            "config": {"workload": "C2: F5TTS_v1_Base CFM.sample, NFE 16 EPSS + sway -1, CFG 2.0, 1 utterance "
+                                   "per GPU, 938 prompt + 938 generated frames (1876), 300 tokens",
+                       "batch_per_gpu": 1, "frames": L, "gen_frames": gen_frames, "nfe": case["nfe"],
+                       "parallelism": f"dp{world}"},
+            "rtf": round(rtf, 5),
+            "path_tflops": round(flops_call * args.steps * world / elapsed / 1e12, 2),
+            "roofline": roof,
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

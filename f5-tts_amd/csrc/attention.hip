@@ -34,36 +34,35 @@ __global__ __launch_bounds__(256, 2) void attn_bf16_kernel(AttnArgs a) {
   bf16x8 qf[4];
 #pragma unroll
   for (int ks = 0; ks < 4; ++ks) {
-    uint4 v = qrow < L ? *reinterpret_cast<const uint4*>(Q + (int64_t)qrow * 64 + ks * 16 + h * 8)
-                       : make_uint4(0, 0, 0, 0);
-    qf[ks] = *reinterpret_cast<bf16x8*>(&v);
+    // rows past L are clamped (their outputs are never stored)
+    uint4 v = *reinterpret_cast<const uint4*>(Q + (int64_t)min(qrow, L - 1) * 64 + ks * 16 + h * 8);
+    qf[ks] = __builtin_bit_cast(bf16x8, v);
   }
 
-  uint4 rk[2], rv[2];
+  // staging registers as named scalars (an array here is lowered to scratch memory)
+  uint4 rk0, rk1, rv0, rv1;
+  const int srow = tid >> 3, sch = tid & 7;  // this thread's chunk: rows srow and srow+32
   auto gload = [&](int kt) {
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      int idx = tid + i * 256, row = idx >> 3, ch = idx & 7;
-      int key = kt * 64 + row;
-      bool ok = key < L;
-      int64_t off = (int64_t)(ok ? key : 0) * 64 + ch * 8;
-      rk[i] = ok ? *reinterpret_cast<const uint4*>(K + off) : make_uint4(0, 0, 0, 0);
-      rv[i] = ok ? *reinterpret_cast<const uint4*>(V + off) : make_uint4(0, 0, 0, 0);
-    }
+    // keys past L are clamped to a real row: their scores are masked (p = 0) below
+    const int64_t o0 = (int64_t)min(kt * 64 + srow, L - 1) * 64 + sch * 8;
+    const int64_t o1 = (int64_t)min(kt * 64 + srow + 32, L - 1) * 64 + sch * 8;
+    rk0 = *reinterpret_cast<const uint4*>(K + o0);
+    rk1 = *reinterpret_cast<const uint4*>(K + o1);
+    rv0 = *reinterpret_cast<const uint4*>(V + o0);
+    rv1 = *reinterpret_cast<const uint4*>(V + o1);
   };
+  const int sw0 = srow * 8 + swz128(srow, sch), sw1 = (srow + 32) * 8 + swz128(srow + 32, sch);
   auto sstore = [&](int buf) {
     uint4* Ks = lds + buf * 1024;
     uint4* Vs = Ks + 512;
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      int idx = tid + i * 256, row = idx >> 3, ch = idx & 7;
-      Ks[row * 8 + swz128(row, ch)] = rk[i];
-      Vs[row * 8 + swz128(row, ch)] = rv[i];
-    }
+    Ks[sw0] = rk0;
+    Ks[sw1] = rk1;
+    Vs[sw0] = rv0;
+    Vs[sw1] = rv1;
   };
 
   const float c = a.scale * 1.4426950408889634f;  // scores in log2 units
-  float m_run = -1e30f, l_run = 0.f;
+  float m_run = -INFINITY, l_run = 0.f;
   f32x16 oacc[2];
 #pragma unroll
   for (int u = 0; u < 2; ++u)
@@ -89,32 +88,44 @@ __global__ __launch_bounds__(256, 2) void attn_bf16_kernel(AttnArgs a) {
       for (int ks = 0; ks < 4; ++ks) {
         int row = t * 32 + (lane & 31);
         uint4 kv = Ks[row * 8 + swz128(row, ks * 2 + h)];
-        sacc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(*reinterpret_cast<bf16x8*>(&kv), qf[ks], sacc[t], 0, 0,
+        sacc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, kv), qf[ks], sacc[t], 0, 0,
                                                            0);
       }
     }
     // ---- online softmax; row (query) on the lane, keys in registers (+ partner lane^32)
-    float mx = -1e30f;
     const int kbase = kt * 64 + 4 * h;
+    const bool full = kt * 64 + 64 <= klen;  // wave-uniform: no key masking needed
+    float mx = -1e30f;
+    if (full) {
 #pragma unroll
-    for (int t = 0; t < 2; ++t)
+      for (int t = 0; t < 2; ++t)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        int key = kbase + t * 32 + (r & 3) + 8 * (r >> 2);
-        float sv = key < klen ? sacc[t][r] * c : -1e30f;
-        sacc[t][r] = sv;
-        mx = fmaxf(mx, sv);
-      }
+        for (int r = 0; r < 16; ++r) {
+          sacc[t][r] *= c;
+          mx = fmaxf(mx, sacc[t][r]);
+        }
+    } else {
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          int key = kbase + t * 32 + (r & 3) + 8 * (r >> 2);
+          float sv = key < klen ? sacc[t][r] * c : -INFINITY;
+          sacc[t][r] = sv;
+          mx = fmaxf(mx, sv);
+        }
+    }
     mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    // the first tile always holds >= 1 valid key, so m_new is finite; exp2(-inf) = 0 for masked keys
     const float m_new = fmaxf(m_run, mx);
-    const float alpha = exp2f(m_run - m_new);
+    const float alpha = __builtin_amdgcn_exp2f(m_run - m_new);
     m_run = m_new;
     float lsum = 0.f;
 #pragma unroll
     for (int t = 0; t < 2; ++t)
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        float p = sacc[t][r] > -1e29f ? exp2f(sacc[t][r] - m_new) : 0.f;
+        float p = __builtin_amdgcn_exp2f(sacc[t][r] - m_new);
         sacc[t][r] = p;
         lsum += p;
       }
@@ -148,8 +159,7 @@ __global__ __launch_bounds__(256, 2) void attn_bf16_kernel(AttnArgs a) {
           const char* a2 = vbytes + r2 * 128 + swz128(r2, chunk) * 16 + half * 8;
           s16x4 v1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_PTR(s16x4))(a1));
           s16x4 v2 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_PTR(s16x4))(a2));
-          short tmp[8] = {v1[0], v1[1], v1[2], v1[3], v2[0], v2[1], v2[2], v2[3]};
-          bf16x8 vf = *reinterpret_cast<bf16x8*>(tmp);
+          bf16x8 vf = __builtin_bit_cast(bf16x8, __builtin_shufflevector(v1, v2, 0, 1, 2, 3, 4, 5, 6, 7));
           oacc[u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf[t][s], oacc[u], 0, 0, 0);
         }
     }

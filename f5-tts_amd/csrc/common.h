@@ -3,6 +3,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 typedef __bf16 bf16;
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
@@ -105,8 +107,19 @@ template <> struct Load16<bf16, float> {
     float4 a = *reinterpret_cast<const float4*>(p);
     float4 b = *reinterpret_cast<const float4*>(p + 4);
     bf16x8 v = {f2bf(a.x), f2bf(a.y), f2bf(a.z), f2bf(a.w), f2bf(b.x), f2bf(b.y), f2bf(b.z), f2bf(b.w)};
-    return *reinterpret_cast<uint4*>(&v);
+    return __builtin_bit_cast(uint4, v);
   }
 };
 
 template <typename T> F5H_DEV constexpr int elems16() { return 16 / (int)sizeof(T); }
+
+// Compile-time loop: f(integral_constant<int, I>) for I in [B, E). Register arrays indexed
+// through it are split into scalars by SROA (a runtime-indexed or loop-indexed array can
+// be lowered to scratch before the unroller runs).
+template <int B, int E, typename F>
+F5H_DEV void static_for(F&& f) {
+  if constexpr (B < E) {
+    f(std::integral_constant<int, B>{});
+    static_for<B + 1, E>(f);
+  }
+}

@@ -36,22 +36,22 @@ __global__ __launch_bounds__(256, 2) void conv_kernel(ConvArgs a) {
     const TX* src = X + ((int64_t)s * L + (ok ? q : 0)) * d + grp * cg + (ok ? ch * E : 0);
     Xs[row * CPR + swz(row, ch)] = Load16<TC, TX>::ld(src, ok);
   }
-  constexpr int WCH = 64 * CPR / 256;  // weight chunks per thread per tap
-  uint4 rw[WCH];
-  auto wload = [&](int t) {
-#pragma unroll
-    for (int i = 0; i < WCH; ++i) {
-      int idx = tid + i * 256, row = idx / CPR, ch = idx % CPR;
-      rw[i] = *reinterpret_cast<const uint4*>(Wg + ((int64_t)t * 64 + row) * 64 + ch * E);
-    }
-  };
-  auto wstore = [&](int buf) {
+  // weight taps stream by LDS-DMA: round r, wave w, lane l -> linear chunk p of the panel;
+  // the swizzle goes on the source chunk so the LDS image is the swz() image (involution)
+  constexpr int WR = CPR / 4;  // DMA rounds per tap (64 rows x CPR chunks / 256 lanes)
+  int woff[WR];
+  static_for<0, WR>([&](auto I) {
+    constexpr int r = decltype(I)::value;
+    const int p = (r * 4 + wid) * 64 + lane, row = p / CPR, slot = p % CPR;
+    woff[r] = row * 64 + swz(row, slot) * E;
+  });
+  auto wdma = [&](int buf, int t) {
     uint4* Ws = Ws0 + buf * 64 * CPR;
-#pragma unroll
-    for (int i = 0; i < WCH; ++i) {
-      int idx = tid + i * 256, row = idx / CPR, ch = idx % CPR;
-      Ws[row * CPR + swz(row, ch)] = rw[i];
-    }
+    static_for<0, WR>([&](auto I) {
+      constexpr int r = decltype(I)::value;
+      __builtin_amdgcn_global_load_lds((const void*)(Wg + (int64_t)t * 64 * 64 + woff[r]),
+                                       (LDS_PTR(void))(Ws + (r * 4 + wid) * 64), 16, 0, 0);
+    });
   };
 
   f32x4 acc[2][2];
@@ -60,39 +60,37 @@ __global__ __launch_bounds__(256, 2) void conv_kernel(ConvArgs a) {
 #pragma unroll
     for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  wload(0);
-  wstore(0);
+  wdma(0, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   for (int t = 0; t < 31; ++t) {
     const int cur = t & 1;
-    if (t + 1 < 31) wload(t + 1);
     const uint4* Ws = Ws0 + cur * 64 * CPR;
+    frag af[CPR / 4][2], bfr[CPR / 4][2];
 #pragma unroll
     for (int sl = 0; sl < CPR / 4; ++sl) {
       const int ch = sl * 4 + (lane >> 4);
-      frag af[2], bfr[2];
 #pragma unroll
       for (int i = 0; i < 2; ++i) {
         int row = wm * 32 + i * 16 + (lane & 15) + t;  // window row of input pos + t - 15
-        uint4 v = Xs[row * CPR + swz(row, ch)];
-        af[i] = *reinterpret_cast<frag*>(&v);
+        af[sl][i] = __builtin_bit_cast(frag, Xs[row * CPR + swz(row, ch)]);
       }
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
         int row = wn * 32 + j * 16 + (lane & 15);
-        uint4 v = Ws[row * CPR + swz(row, ch)];
-        bfr[j] = *reinterpret_cast<frag*>(&v);
+        bfr[sl][j] = __builtin_bit_cast(frag, Ws[row * CPR + swz(row, ch)]);
       }
+    }
+    if (t + 1 < 31) wdma(cur ^ 1, t + 1);
+#pragma unroll
+    for (int sl = 0; sl < CPR / 4; ++sl)
 #pragma unroll
       for (int i = 0; i < 2; ++i)
 #pragma unroll
-        for (int j = 0; j < 2; ++j) acc[i][j] = Slab<TC>::mma(af[i], bfr[j], acc[i][j]);
-    }
-    if (t + 1 < 31) {
-      __syncthreads();
-      wstore(cur ^ 1);
-      __syncthreads();
-    }
+        for (int j = 0; j < 2; ++j) acc[i][j] = Slab<TC>::mma(af[sl][i], bfr[sl][j], acc[i][j]);
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
   }
 
 #pragma unroll

@@ -41,12 +41,16 @@ hipError_t time_sinus(const float* t_host, int n, float* out, hipStream_t st) {
   return hipGetLastError();
 }
 
-__global__ void silu_kernel(const float* x, float* y, int64_t n) {
+template <typename TO>
+__global__ void silu_kernel(const float* x, TO* y, int64_t n) {
   int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < n) y[i] = silu(x[i]);
+  if (i < n) y[i] = from_f32<TO>(silu(x[i]));
 }
-hipError_t silu_inplace_copy(const float* x, float* y, int64_t n, hipStream_t st) {
-  hipLaunchKernelGGL(silu_kernel, dim3(nblk(n, 256)), dim3(256), 0, st, x, y, n);
+hipError_t silu_to_op(int compute, const float* x, void* y, int64_t n, hipStream_t st) {
+  if (compute)
+    hipLaunchKernelGGL(silu_kernel<bf16>, dim3(nblk(n, 256)), dim3(256), 0, st, x, (bf16*)y, n);
+  else
+    hipLaunchKernelGGL(silu_kernel<float>, dim3(nblk(n, 256)), dim3(256), 0, st, x, (float*)y, n);
   return hipGetLastError();
 }
 

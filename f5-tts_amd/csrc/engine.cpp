@@ -332,7 +332,8 @@ struct WS {
 };
 
 struct Bufs {
-  float *tsin, *th, *temb, *tsilu, *ada;
+  float *tsin, *th, *temb, *ada;
+  void* tin_op;
   float *te, *pw1o, *grn_scr;
   void *dwln, *grno;
   uint8_t* keepfill;
@@ -344,7 +345,7 @@ struct Bufs {
   float2* rope;
   uint8_t* rowkeep;
   int32_t* kvlen;
-  std::vector<float*> skips;
+  std::vector<void*> skips;
 };
 
 static void layout(const f5h_engine* e, WS& ws, Bufs& b, int B, int N, int nfe, int use_cfg) {
@@ -356,7 +357,7 @@ static void layout(const f5h_engine* e, WS& ws, Bufs& b, int B, int N, int nfe, 
   b.tsin = ws.take<float>((size_t)nfe * 256);
   b.th = ws.take<float>((size_t)nfe * d);
   b.temb = ws.take<float>((size_t)nfe * d);
-  b.tsilu = ws.take<float>((size_t)nfe * d);
+  b.tin_op = ws.take<char>((size_t)nfe * std::max(256, d) * es);
   b.ada = a.backbone == F5H_DIT ? ws.take<float>((size_t)nfe * e->ada.Npad) : nullptr;
   b.te = ws.take<float>((size_t)2 * B * N * td);
   b.keepfill = ws.take<uint8_t>((size_t)2 * B * N);
@@ -388,7 +389,7 @@ static void layout(const f5h_engine* e, WS& ws, Bufs& b, int B, int N, int nfe, 
   b.kvlen = ws.take<int32_t>(S);
   b.skips.clear();
   if (a.backbone == F5H_UNETT)
-    for (int i = 0; i < a.depth / 2; ++i) b.skips.push_back(ws.take<float>(rows * d));
+    for (int i = 0; i < a.depth / 2; ++i) b.skips.push_back(ws.take<char>(rows * d * es));
 }
 
 // ---------------------------------------------------------------- probe
@@ -469,14 +470,16 @@ static int prologue(Ctx& c, const float* t_host, int nt_vals, const float* cond,
   // ---- time embedding for every grid point used, then the AdaLN table
   {
     KCK(time_sinus(t_host, nt_vals, b.tsin, st));
-    GemmArgs g = gargs(b.tsin, 256, e->t1, nt_vals, b.th, d);
-    KCK(gemm(bf, true, EPI_SILU, g, st));
-    g = gargs(b.th, d, e->t2, nt_vals, b.temb, d);
-    KCK(gemm(bf, true, EPI_STORE, g, st));
+    KCK(f32_to_op(bf, b.tsin, (int64_t)nt_vals * 256, b.tin_op, st));
+    GemmArgs g = gargs(b.tin_op, 256, e->t1, nt_vals, b.th, d);
+    KCK(gemm(bf, EPI_SILU, g, st));
+    KCK(f32_to_op(bf, b.th, (int64_t)nt_vals * d, b.tin_op, st));
+    g = gargs(b.tin_op, d, e->t2, nt_vals, b.temb, d);
+    KCK(gemm(bf, EPI_STORE, g, st));
     if (a.backbone == F5H_DIT) {
-      KCK(silu_inplace_copy(b.temb, b.tsilu, (int64_t)nt_vals * d, st));
-      g = gargs(b.tsilu, d, e->ada, nt_vals, b.ada, e->ada.Npad);
-      KCK(gemm(bf, true, EPI_STORE, g, st));
+      KCK(silu_to_op(bf, b.temb, b.tin_op, (int64_t)nt_vals * d, st));
+      g = gargs(b.tin_op, d, e->ada, nt_vals, b.ada, e->ada.Npad);
+      KCK(gemm(bf, EPI_STORE, g, st));
     }
   }
   // ---- text embedding, both branches (cached once per call in the reference, dit.py:294-310)
@@ -500,17 +503,17 @@ static int prologue(Ctx& c, const float* t_host, int nt_vals, const float* cond,
       CNX& x = e->cnx[i];
       KCK(dwconv_ln(bf, b.te, S2, c.N, td, x.dw_w, x.dw_b, x.ln_w, x.ln_b, b.dwln, st));
       GemmArgs g = gargs(b.dwln, td, x.pw1, R2, b.pw1o, 2 * td);
-      KCK(gemm(bf, false, EPI_GELU_ERF, g, st));
+      KCK(gemm(bf, EPI_GELU_ERF, g, st));
       KCK(grn(bf, b.pw1o, S2, c.N, 2 * td, x.gamma, x.beta, b.grn_scr, b.grno, st));
       g = gargs(b.grno, 2 * td, x.pw2, R2, b.te, td);
       g.rowkeep = a.text_mask_padding ? b.keepfill : nullptr;
-      KCK(gemm(bf, false, EPI_RESID_FILL, g, st));
+      KCK(gemm(bf, EPI_RESID_FILL, g, st));
     }
   }
   // ---- hoisted input projection: P = [step_cond | text] . W_ct^T + b
   KCK(build_ct(bf, cond, cond_mask, b.te, b.te + (size_t)c.B * c.N * td, c.B, c.N, td, c.S, b.act, st));
   GemmArgs g = gargs(b.act, 128 + e->tdp, e->in_ct, c.S * c.N, b.P, d);
-  KCK(gemm(bf, false, EPI_STORE, g, st));
+  KCK(gemm(bf, EPI_STORE, g, st));
   return 0;
 }
 
@@ -532,7 +535,7 @@ static int backbone_step(Ctx& c, int k) {
     g.add = b.P;
     g.ld_add = d;
     g.dual_rows = c.use_cfg ? BN : 0;
-    KCK(gemm(bf, false, EPI_INPROJ, g, st));
+    KCK(gemm(bf, EPI_INPROJ, g, st));
     ConvArgs cv{};
     cv.S = c.S;
     cv.L = c.N;
@@ -569,12 +572,15 @@ static int backbone_step(Ctx& c, int k) {
     const float* ad = ada_k ? ada_k + (size_t)l * 6 * d : nullptr;
     if (!dit) {
       if (l < a.depth / 2) {
-        KCK(hipMemcpyAsync(b.skips[l], h, (size_t)rows * d * sizeof(float), hipMemcpyDeviceToDevice, st));
+        // skips are only ever GEMM A operands: keep them in the operand dtype
+        KCK(f32_to_op(bf, h, (int64_t)rows * d, b.skips[l], st));
       } else {
-        GemmArgs g = gargs(h, d, Ly.skip1, rows, h2, d);
-        KCK(gemm(bf, true, EPI_STORE, g, st));
+        // skip_proj(cat(x, skip)) = x.W1^T + skip.W2^T (unett.py:288-297)
+        KCK(f32_to_op(bf, h, (int64_t)rows * d, b.aop, st));
+        GemmArgs g = gargs(b.aop, d, Ly.skip1, rows, h2, d);
+        KCK(gemm(bf, EPI_STORE, g, st));
         g = gargs(b.skips[a.depth - 1 - l], d, Ly.skip2, rows, h2, d);
-        KCK(gemm(bf, true, EPI_RESID, g, st));
+        KCK(gemm(bf, EPI_RESID, g, st));
         std::swap(h, h2);
       }
       KCK(rms_norm_g(bf, h, rows, d, Ly.g_attn, b.aop, st));
@@ -591,7 +597,7 @@ static int backbone_step(Ctx& c, int k) {
       g.k = b.k;
       g.v = b.v;
       ProbeScope ps(e, KC_QKV, st);
-      KCK(gemm(bf, false, EPI_QKV, g, st));
+      KCK(gemm(bf, EPI_QKV, g, st));
     }
     {
       AttnArgs at{};
@@ -611,7 +617,7 @@ static int backbone_step(Ctx& c, int k) {
       GemmArgs g = gargs(b.o, inner, Ly.out, rows, h, d);
       g.gate = ad ? ad + 2 * d : nullptr;  // gate_msa
       g.rowkeep = keep;                    // masked_fill of pad rows (modules.py:552-554)
-      KCK(gemm(bf, false, EPI_RESID, g, st));
+      KCK(gemm(bf, EPI_RESID, g, st));
     }
     if (dit)
       KCK(ln_modulate(bf, h, rows, d, ad + 3 * d /*shift_mlp*/, ad + 4 * d /*scale_mlp*/, b.aop, st));
@@ -620,13 +626,13 @@ static int backbone_step(Ctx& c, int k) {
     {
       GemmArgs g = gargs(b.aop, d, Ly.ff1, rows, b.f, a.ff_dim);
       ProbeScope ps(e, KC_FFN1, st);
-      KCK(gemm(bf, false, EPI_GELU_TANH, g, st));
+      KCK(gemm(bf, EPI_GELU_TANH, g, st));
     }
     {
       GemmArgs g = gargs(b.f, a.ff_dim, Ly.ff2, rows, h, d);
       g.gate = ad ? ad + 5 * d : nullptr;  // gate_mlp
       ProbeScope ps(e, KC_FFN2, st);
-      KCK(gemm(bf, false, EPI_RESID, g, st));
+      KCK(gemm(bf, EPI_RESID, g, st));
     }
   }
   if (dit) {
@@ -636,7 +642,7 @@ static int backbone_step(Ctx& c, int k) {
     KCK(rms_norm_g(bf, h, rows, d, e->norm_out_g, b.aop, st));
   }
   GemmArgs g = gargs(b.aop, d, e->proj_out, rows, b.p, a.mel_dim);
-  KCK(gemm(bf, false, EPI_STORE, g, st));
+  KCK(gemm(bf, EPI_STORE, g, st));
   return 0;
 }
 
@@ -819,12 +825,19 @@ int f5h_op_linear(void* stream, int32_t compute, int32_t M, int32_t N, int32_t K
   const int Npad = (N + 127) / 128 * 128;
   const size_t es = compute ? 2 : 4;
   const size_t need = (size_t)Npad * K * es;
-  if (workspace_bytes < need) return fail(F5H_ENOMEM, "workspace too small for op_linear");
+  if (workspace_bytes < (need + 255) / 256 * 256 + (size_t)M * K * es)
+    return fail(F5H_ENOMEM, "workspace too small for op_linear");
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   HIPCK(hipMemsetAsync(workspace, 0, need, st));
   HIPCK(f32_to_op(compute, W, (int64_t)N * K, workspace, st));
+  const void* Aop = A;
+  if (compute) {
+    char* ab = reinterpret_cast<char*>(workspace) + (need + 255) / 256 * 256;
+    HIPCK(f32_to_op(compute, A, (int64_t)M * K, ab, st));
+    Aop = ab;
+  }
   GemmArgs g{};
-  g.A = A;
+  g.A = Aop;
   g.lda = K;
   g.W = workspace;
   g.ldw = K;
@@ -834,7 +847,7 @@ int f5h_op_linear(void* stream, int32_t compute, int32_t M, int32_t N, int32_t K
   g.bias = bias;
   g.C = C;
   g.ldc = N;
-  HIPCK(gemm(compute, true, EPI_STORE, g, st));
+  HIPCK(gemm(compute, EPI_STORE, g, st));
   return 0;
 }
 

@@ -33,8 +33,8 @@ struct GemmArgs {
   void* q; void* k; void* v;
 };
 
-// compute: 0 fp32 operands, 1 bf16 operands. a_f32: A is fp32 in memory (converted on load).
-hipError_t gemm(int compute, bool a_f32, int epi, const GemmArgs& a, hipStream_t st);
+// compute: 0 fp32 operands, 1 bf16 operands. A and W both in the operand dtype.
+hipError_t gemm(int compute, int epi, const GemmArgs& a, hipStream_t st);
 
 // attention: Q,K,V [S,H,L,64] operand dtype; O [S,L,H*64] operand dtype.
 struct AttnArgs {
@@ -61,7 +61,7 @@ hipError_t conv_pos(int compute, const ConvArgs& a, hipStream_t st);
 
 // ---- elementwise / small kernels (elementwise.hip)
 hipError_t time_sinus(const float* t_host, int n, float* out, hipStream_t st);  // host t[n<=512] -> [n,256]
-hipError_t silu_inplace_copy(const float* x, float* y, int64_t n, hipStream_t st);
+hipError_t silu_to_op(int compute, const float* x, void* y, int64_t n, hipStream_t st);
 // LayerNorm(no affine, eps) * (1 + scale) + shift -> operand dtype; h: [M, d] fp32
 hipError_t ln_modulate(int compute, const float* h, int M, int d, const float* shift, const float* scale,
                        void* out, hipStream_t st);

@@ -161,7 +161,7 @@ def op_linear(A, W, bias=None, compute="bf16"):
     M, K = A.shape
     N = W.shape[0]
     C = torch.empty(M, N, dtype=torch.float32, device=A.device)
-    ws = torch.empty(((N + 127) // 128 * 128) * K * 4 + 256, dtype=torch.uint8, device=A.device)
+    ws = torch.empty(((N + 127) // 128 * 128) * K * 4 + 512 + M * K * 4, dtype=torch.uint8, device=A.device)
     c = {"fp32": 0, "bf16": 1}[compute]
     _lib.check(_lib.lib().f5h_op_linear(_lib.stream_handle(A.device), c, M, N, K, A.contiguous().data_ptr(),
                                         W.contiguous().data_ptr(), _lib.ptr(bias), C.data_ptr(), ws.data_ptr(),
