@@ -15,6 +15,7 @@
 
 namespace f5h {
 
+template <bool PRESCALED>
 __global__ __launch_bounds__(256, 2) void attn_bf16_kernel(AttnArgs a) {
   __shared__ __attribute__((aligned(16))) uint4 lds[2 * 2 * 64 * 8];  // [buf][K|V][64 rows][8 chunks]
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
@@ -61,7 +62,7 @@ __global__ __launch_bounds__(256, 2) void attn_bf16_kernel(AttnArgs a) {
     Vs[sw1] = rv1;
   };
 
-  const float c = a.scale * 1.4426950408889634f;  // scores in log2 units
+  const float c = a.scale * 1.4426950408889634f;  // scores in log2 units (unless q carries it)
   float m_run = -INFINITY, l_run = 0.f;
   f32x16 oacc[2];
 #pragma unroll
@@ -101,7 +102,7 @@ __global__ __launch_bounds__(256, 2) void attn_bf16_kernel(AttnArgs a) {
       for (int t = 0; t < 2; ++t)
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-          sacc[t][r] *= c;
+          if constexpr (!PRESCALED) sacc[t][r] *= c;
           mx = fmaxf(mx, sacc[t][r]);
         }
     } else {
@@ -110,7 +111,7 @@ __global__ __launch_bounds__(256, 2) void attn_bf16_kernel(AttnArgs a) {
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           int key = kbase + t * 32 + (r & 3) + 8 * (r >> 2);
-          float sv = key < klen ? sacc[t][r] * c : -INFINITY;
+          float sv = key < klen ? (PRESCALED ? sacc[t][r] : sacc[t][r] * c) : -INFINITY;
           sacc[t][r] = sv;
           mx = fmaxf(mx, sv);
         }
@@ -130,10 +131,12 @@ __global__ __launch_bounds__(256, 2) void attn_bf16_kernel(AttnArgs a) {
         lsum += p;
       }
     l_run = l_run * alpha + lsum;
+    if (!__all(alpha == 1.f)) {  // running max moved for some row: rescale (exact skip otherwise)
 #pragma unroll
-    for (int u = 0; u < 2; ++u)
+      for (int u = 0; u < 2; ++u)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) oacc[u][r] *= alpha;
+        for (int r = 0; r < 16; ++r) oacc[u][r] *= alpha;
+    }
 
     // ---- O^T += V^T P^T
     bf16x8 pf[2][2];
@@ -222,17 +225,17 @@ __global__ __launch_bounds__(64) void attn_f32_kernel(AttnArgs a) {
       float acc = 0.f;
 #pragma unroll
       for (int d = 0; d < 64; ++d) acc = fmaf(q[d], Ks[r][d], acc);
-      sc[r] = (k0 + r < klen) ? acc * a.scale : -INFINITY;
+      sc[r] = (k0 + r < klen) ? (a.prescaled ? acc : acc * a.scale) : -INFINITY;
       mx = fmaxf(mx, sc[r]);
     }
-    const float alpha = expf(m_run - mx);
+    const float alpha = a.prescaled ? exp2f(m_run - mx) : expf(m_run - mx);
     m_run = mx;
     l_run *= alpha;
 #pragma unroll
     for (int d = 0; d < 64; ++d) o[d] *= alpha;
 #pragma unroll
     for (int r = 0; r < 32; ++r) {
-      float p = expf(sc[r] - mx);
+      float p = a.prescaled ? exp2f(sc[r] - mx) : expf(sc[r] - mx);
       l_run += p;
 #pragma unroll
       for (int d = 0; d < 64; ++d) o[d] = fmaf(p, Vs[r][d], o[d]);
@@ -250,7 +253,10 @@ hipError_t attention(int compute, const AttnArgs& a, hipStream_t st) {
   if (a.S <= 0 || a.H <= 0 || a.L <= 0) return hipErrorInvalidValue;
   if (compute) {
     dim3 grid((a.L + 127) / 128, a.S * a.H);
-    hipLaunchKernelGGL(attn_bf16_kernel, grid, dim3(256), 0, st, a);
+    if (a.prescaled)
+      hipLaunchKernelGGL(attn_bf16_kernel<true>, grid, dim3(256), 0, st, a);
+    else
+      hipLaunchKernelGGL(attn_bf16_kernel<false>, grid, dim3(256), 0, st, a);
   } else {
     dim3 grid((a.L + 63) / 64, a.S * a.H);
     hipLaunchKernelGGL(attn_f32_kernel, grid, dim3(64), 0, st, a);

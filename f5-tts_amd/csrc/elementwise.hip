@@ -246,26 +246,36 @@ hipError_t dwconv_ln(int compute, const float* x, int S, int L, int C, const flo
 
 // GRN (modules.py:236-245): Gx = ||x||_2 over the TIME axis, Nx = Gx / (mean_c Gx + 1e-6),
 // out = gamma * (x * Nx) + beta + x
-__global__ void grn_sumsq_kernel(const float* x, int L, int C, float* sumsq) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x, s = blockIdx.y;
+// Deterministic two-stage column reduction: partial[z][s][c] over 64-row chunks, then a
+// fixed-order sum (no float atomics: results must not depend on arrival order).
+__global__ void grn_sumsq_kernel(const float* x, int S, int L, int C, float* partial) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x, s = blockIdx.y, z = blockIdx.z;
   if (c >= C) return;
+  const int n0 = z * 64, n1 = min(L, n0 + 64);
   float acc = 0.f;
-  for (int n = 0; n < L; ++n) {
+  for (int n = n0; n < n1; ++n) {
     float v = x[((int64_t)s * L + n) * C + c];
     acc += v * v;
   }
-  sumsq[(int64_t)s * C + c] = sqrtf(acc);
+  partial[((int64_t)z * S + s) * C + c] = acc;
 }
-__global__ void grn_norm_kernel(float* gx, int C) {
+// nx[s][c] = Gx / (mean_c Gx + 1e-6), Gx = sqrt(sum_z partial)
+__global__ void grn_norm_kernel(const float* partial, int nz, int S, int C, float* nx) {
   const int s = blockIdx.x;
   float acc = 0.f;
-  for (int c = threadIdx.x; c < C; c += 256) acc += gx[(int64_t)s * C + c];
+  for (int c = threadIdx.x; c < C; c += 256) {
+    float ss = 0.f;
+    for (int z = 0; z < nz; ++z) ss += partial[((int64_t)z * S + s) * C + c];
+    const float g = sqrtf(ss);  // ||x||_2 over time
+    nx[(int64_t)s * C + c] = g;
+    acc += g;
+  }
   __shared__ float red[4];
   acc = wave_sum(acc);
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
   __syncthreads();
   const float mean = (red[0] + red[1] + red[2] + red[3]) / C;
-  for (int c = threadIdx.x; c < C; c += 256) gx[(int64_t)s * C + c] = gx[(int64_t)s * C + c] / (mean + 1e-6f);
+  for (int c = threadIdx.x; c < C; c += 256) nx[(int64_t)s * C + c] = nx[(int64_t)s * C + c] / (mean + 1e-6f);
 }
 template <typename TO>
 __global__ void grn_apply_kernel(const float* x, int L, int C, const float* nx, const float* gamma,
@@ -279,8 +289,12 @@ __global__ void grn_apply_kernel(const float* x, int L, int C, const float* nx, 
 }
 hipError_t grn(int compute, const float* x, int S, int L, int C, const float* gamma, const float* beta,
                float* scratch, void* out, hipStream_t st) {
-  hipLaunchKernelGGL(grn_sumsq_kernel, dim3(nblk(C, 256), S), dim3(256), 0, st, x, L, C, scratch);
-  hipLaunchKernelGGL(grn_norm_kernel, dim3(S), dim3(256), 0, st, scratch, C);
+  // scratch: [nz*S*C] partials then [S*C] normalisers
+  const int nz = (int)nblk(L, 64);
+  float* nx = scratch + (size_t)nz * S * C;
+  hipLaunchKernelGGL(grn_sumsq_kernel, dim3(nblk(C, 256), S, nz), dim3(256), 0, st, x, S, L, C, scratch);
+  hipLaunchKernelGGL(grn_norm_kernel, dim3(S), dim3(256), 0, st, scratch, nz, S, C, nx);
+  scratch = nx;
   const int64_t total = (int64_t)S * L * C;
   if (compute)
     hipLaunchKernelGGL(grn_apply_kernel<bf16>, dim3(nblk(total, 256)), dim3(256), 0, st, x, L, C, scratch, gamma,

@@ -365,7 +365,7 @@ static void layout(const f5h_engine* e, WS& ws, Bufs& b, int B, int N, int nfe, 
     b.dwln = ws.take<char>((size_t)2 * B * N * td * es);
     b.pw1o = ws.take<float>((size_t)2 * B * N * 2 * td);
     b.grno = ws.take<char>((size_t)2 * B * N * 2 * td * es);
-    b.grn_scr = ws.take<float>((size_t)2 * B * 2 * td);
+    b.grn_scr = ws.take<float>((size_t)((N + 63) / 64 + 1) * 2 * B * 2 * td);
   } else {
     b.dwln = b.grno = nullptr;
     b.pw1o = b.grn_scr = nullptr;
@@ -596,6 +596,7 @@ static int backbone_step(Ctx& c, int k) {
       g.q = b.q;
       g.k = b.k;
       g.v = b.v;
+      g.q_scale = 0.125f * 1.4426950408889634f;  // softmax scale 1/sqrt(64) in log2 units, folded into q
       ProbeScope ps(e, KC_QKV, st);
       KCK(gemm(bf, EPI_QKV, g, st));
     }
@@ -610,6 +611,7 @@ static int backbone_step(Ctx& c, int k) {
       at.L = c.L;
       at.kv_len = (a.attn_mask_enabled && c.batch_mask) ? b.kvlen : nullptr;
       at.scale = 0.125f;
+      at.prescaled = 1;
       ProbeScope ps(e, KC_ATTN, st);
       KCK(attention(bf, at, st));
     }

@@ -6,132 +6,234 @@
 // (dit.py:162), proj_out (dit.py:368), the all-steps AdaLN table (modules.py:321-323) and
 // the ConvNeXt pointwise convs (modules.py:265-269).
 //
-// Tiling: 256 threads = 4 waves as 2x2, block tile BM x BN, K staged 128 bytes per row
-// per stage (64 bf16 / 32 fp32) by LDS-DMA (global_load_lds) into a double-buffered,
+// Main loop: 256 threads = 4 waves as 2x2, block tile BM x 128 (BM = 128, or 64 when the
+// 128-row grid would leave CUs without a second block), K staged 128 bytes per row per
+// stage (64 bf16 / 32 fp32) by LDS-DMA (global_load_lds) into a double-buffered,
 // XOR-swizzled LDS image; A and W are both K-contiguous operand-dtype panels, so every
-// fragment is one ds_read_b128. fp32 activations are converted to the operand dtype by
-// the producer (or f32_to_op) before they reach a GEMM.
-// bf16 mode: v_mfma_f32_16x16x32_bf16; fp32 parity mode: v_mfma_f32_16x16x4_f32 (exact f32).
+// fragment is one ds_read_b128. bf16 mode: v_mfma_f32_16x16x32_bf16; fp32 parity mode:
+// v_mfma_f32_16x16x4_f32 (exact f32).
+// Epilogue: the fp32 accumulator tile is staged through LDS (padded rows) and re-read
+// row-contiguously, so every global access of the epilogue (bias, gate, residual, RoPE
+// table, q/k/v scatter) is a 16-32 byte vector access on whole rows.
 #include "common.h"
 #include "kernels.h"
 
-#include <type_traits>
+#include <cstdlib>
 
 namespace f5h {
 
-// ------------------------------------------------------------ epilogue (shared by both kernels)
-// C layout (16x16 MFMA): col = lane&15, row = (lane>>4)*4 + r
-template <typename TC, int EPI, int BM, int BN>
-F5H_DEV void epilogue(const GemmArgs& g, f32x4 (&acc)[BM / 32][BN / 32], int m0, int n0, int wm, int wn, int lane) {
-  constexpr int WM = BM / 2, WN = BN / 2, MT = WM / 16, NT = WN / 16;
+constexpr int GBN = 128;         // block tile columns
+constexpr int CPAD = GBN + 4;    // fp32 epilogue staging row (528 B: conflict-free MFMA-layout writes)
+
+template <int BM>
+struct GemmLds {
+  static constexpr int stage_bytes = (BM + GBN) * 128;
+  static constexpr int main_bytes = 3 * stage_bytes;
+  static constexpr int epi_bytes = BM * CPAD * 4;
+  static constexpr int bytes = main_bytes > epi_bytes ? main_bytes : epi_bytes;
+};
+
+// ds_read_b128 the compiler does not see (no waitcnt bookkeeping): the caller waits lgkmcnt itself
+template <int OFF>
+F5H_DEV u32x4 lds_read_b128(uint32_t addr) {
+  u32x4 r;
+  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(r) : "v"(addr), "i"(OFF));
+  return r;
+}
+
+// 8 consecutive fp32 values of one row
+struct V8 {
+  float v[8];
+};
+
+template <typename TC>
+F5H_DEV void store8(TC* p, const V8& x);
+template <>
+F5H_DEV void store8<float>(float* p, const V8& x) {
+  *reinterpret_cast<float4*>(p) = make_float4(x.v[0], x.v[1], x.v[2], x.v[3]);
+  *reinterpret_cast<float4*>(p + 4) = make_float4(x.v[4], x.v[5], x.v[6], x.v[7]);
+}
+template <>
+F5H_DEV void store8<bf16>(bf16* p, const V8& x) {
+  bf16x8 b = {f2bf(x.v[0]), f2bf(x.v[1]), f2bf(x.v[2]), f2bf(x.v[3]),
+              f2bf(x.v[4]), f2bf(x.v[5]), f2bf(x.v[6]), f2bf(x.v[7])};
+  *reinterpret_cast<bf16x8*>(p) = b;
+}
+F5H_DEV V8 load8(const float* p) {
+  float4 a = *reinterpret_cast<const float4*>(p), b = *reinterpret_cast<const float4*>(p + 4);
+  return V8{{a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w}};
+}
+
+// Apply the epilogue to 8 consecutive columns [col, col+8) of output row `row`.
+template <typename TC, int EPI>
+F5H_DEV void epi8(const GemmArgs& g, int row, int col, V8 x) {
+  const bool full = col + 8 <= g.N;
+  if (g.bias) {
+    if (full) {
+      V8 b = load8(g.bias + col);
 #pragma unroll
-  for (int i = 0; i < MT; ++i) {
+      for (int e = 0; e < 8; ++e) x.v[e] += b.v[e];
+    } else {
 #pragma unroll
-    for (int j = 0; j < NT; ++j) {
-      const int col = n0 + wn * WN + j * 16 + (lane & 15);
-      const bool cok = col < g.N;
-      const float b = (g.bias && cok) ? g.bias[col] : 0.f;
+      for (int e = 0; e < 8; ++e) x.v[e] += col + e < g.N ? g.bias[col + e] : 0.f;
+    }
+  }
+  if constexpr (EPI == EPI_QKV) {
+    // interleaved RoPE pairs (2i, 2i+1) (x_transformers rotate_half) never straddle an 8-column chunk;
+    // a 64-column head maps to one contiguous 128 B row segment of q/k/v [S,H,L,64]
+    const int inner = g.heads * 64;
+    const int which = col / inner, hc = col - which * inner;
+    const int head = hc >> 6, dh = hc & 63;
+    const int s = row / g.seq_len, pos = row - s * g.seq_len;
+    if (which < 2 && head < g.rope_heads) {
+      const float4* cs = reinterpret_cast<const float4*>(g.rope + (int64_t)pos * 32 + (dh >> 1));
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int row = m0 + wm * WM + i * 16 + (lane >> 4) * 4 + r;
-        const bool ok = cok && row < g.M;
-        float v = acc[i][j][r] + b;
-        if constexpr (EPI == EPI_QKV) {
-          // interleaved RoPE pairs (2i, 2i+1) sit in adjacent lanes (x_transformers rotate_half)
-          float pv = __shfl_xor(v, 1, 64);
-          const int inner = g.heads * 64;
-          const int which = col / inner, hc = col - which * inner;
-          const int head = hc >> 6, dh = hc & 63;
-          const int s = row / g.seq_len, pos = row - s * g.seq_len;
-          if (ok) {
-            if (which < 2 && head < g.rope_heads) {
-              float2 cs = g.rope[(int64_t)pos * 32 + (dh >> 1)];
-              v = (dh & 1) ? (v * cs.x + pv * cs.y) : (v * cs.x - pv * cs.y);
-            }
-            TC* dst = reinterpret_cast<TC*>(which == 0 ? g.q : (which == 1 ? g.k : g.v));
-            dst[(((int64_t)s * g.heads + head) * g.seq_len + pos) * 64 + dh] = from_f32<TC>(v);
-          }
-        } else {
-          if (!ok) continue;
-          const int64_t off = (int64_t)row * g.ldc + col;
-          if constexpr (EPI == EPI_STORE) {
-            reinterpret_cast<float*>(g.C)[off] = v;
-          } else if constexpr (EPI == EPI_SILU) {
-            reinterpret_cast<float*>(g.C)[off] = silu(v);
-          } else if constexpr (EPI == EPI_GELU_TANH) {
-            reinterpret_cast<TC*>(g.C)[off] = from_f32<TC>(gelu_tanh(v));
-          } else if constexpr (EPI == EPI_GELU_ERF) {
-            reinterpret_cast<float*>(g.C)[off] = gelu_erf(v);
-          } else if constexpr (EPI == EPI_RESID) {
-            float gt = g.gate ? g.gate[col] : 1.f;
-            float keep = (g.rowkeep && !g.rowkeep[row]) ? 0.f : 1.f;
-            float* C = reinterpret_cast<float*>(g.C);
-            C[off] = C[off] + gt * (v * keep);
-          } else if constexpr (EPI == EPI_RESID_FILL) {
-            float* C = reinterpret_cast<float*>(g.C);
-            bool keep = !g.rowkeep || g.rowkeep[row];
-            C[off] = keep ? C[off] + v : 0.f;
-          } else if constexpr (EPI == EPI_INPROJ) {
-            float* C = reinterpret_cast<float*>(g.C);
-            const int64_t ao = (int64_t)row * g.ld_add + col;
-            C[off] = v + g.add[ao];
-            if (g.dual_rows) C[off + g.dual_rows * g.ldc] = v + g.add[ao + g.dual_rows * g.ld_add];
-          }
-        }
+      for (int pr = 0; pr < 2; ++pr) {
+        float4 c2 = cs[pr];  // (cos, sin) of two consecutive pairs
+        float a0 = x.v[4 * pr + 0], a1 = x.v[4 * pr + 1], b0 = x.v[4 * pr + 2], b1 = x.v[4 * pr + 3];
+        x.v[4 * pr + 0] = a0 * c2.x - a1 * c2.y;
+        x.v[4 * pr + 1] = a1 * c2.x + a0 * c2.y;
+        x.v[4 * pr + 2] = b0 * c2.z - b1 * c2.w;
+        x.v[4 * pr + 3] = b1 * c2.z + b0 * c2.w;
       }
+    }
+    if (which == 0 && g.q_scale != 0.f) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) x.v[e] *= g.q_scale;
+    }
+    TC* dst = reinterpret_cast<TC*>(which == 0 ? g.q : (which == 1 ? g.k : g.v));
+    store8<TC>(dst + (((int64_t)s * g.heads + head) * g.seq_len + pos) * 64 + dh, x);
+    return;
+  }
+  const int64_t off = (int64_t)row * g.ldc + col;
+  const bool vec = full && (g.ldc % 4 == 0);
+  if constexpr (EPI == EPI_GELU_TANH) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) x.v[e] = gelu_tanh(x.v[e]);
+    TC* C = reinterpret_cast<TC*>(g.C);
+    if (full && g.ldc % 8 == 0) {
+      store8<TC>(C + off, x);
+    } else {
+      for (int e = 0; e < 8; ++e)
+        if (col + e < g.N) C[off + e] = from_f32<TC>(x.v[e]);
+    }
+    return;
+  } else {
+    float* C = reinterpret_cast<float*>(g.C);
+    if constexpr (EPI == EPI_SILU) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) x.v[e] = silu(x.v[e]);
+    } else if constexpr (EPI == EPI_GELU_ERF) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) x.v[e] = gelu_erf(x.v[e]);
+    } else if constexpr (EPI == EPI_RESID) {
+      const float keep = (g.rowkeep && !g.rowkeep[row]) ? 0.f : 1.f;
+      V8 c = vec ? load8(C + off) : V8{};
+      if (!vec)
+        for (int e = 0; e < 8; ++e) c.v[e] = col + e < g.N ? C[off + e] : 0.f;
+      V8 gt = g.gate ? (full ? load8(g.gate + col) : V8{}) : V8{{1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f}};
+      if (g.gate && !full)
+        for (int e = 0; e < 8; ++e) gt.v[e] = col + e < g.N ? g.gate[col + e] : 0.f;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) x.v[e] = c.v[e] + gt.v[e] * (x.v[e] * keep);
+    } else if constexpr (EPI == EPI_RESID_FILL) {
+      const bool keep = !g.rowkeep || g.rowkeep[row];
+      V8 c = vec ? load8(C + off) : V8{};
+      if (!vec)
+        for (int e = 0; e < 8; ++e) c.v[e] = col + e < g.N ? C[off + e] : 0.f;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) x.v[e] = keep ? c.v[e] + x.v[e] : 0.f;
+    } else if constexpr (EPI == EPI_INPROJ) {
+      const int64_t ao = (int64_t)row * g.ld_add + col;
+      V8 a0 = load8(g.add + ao);
+      V8 o0, o1;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) o0.v[e] = x.v[e] + a0.v[e];
+      store8<float>(C + off, o0);
+      if (g.dual_rows) {
+        V8 a1 = load8(g.add + ao + g.dual_rows * g.ld_add);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) o1.v[e] = x.v[e] + a1.v[e];
+        store8<float>(C + off + g.dual_rows * g.ldc, o1);
+      }
+      return;
+    }
+    if (vec) {
+      store8<float>(C + off, x);
+    } else {
+      for (int e = 0; e < 8; ++e)
+        if (col + e < g.N) C[off + e] = x.v[e];
     }
   }
 }
 
-// ---------------------------------------------------------------- LDS-DMA (global_load_lds) variant
-// A and W both in operand dtype: each wave-instruction DMAs 64 x 16 B straight into LDS at
-// (wave-uniform base + lane*16); the XOR swizzle is applied to the per-lane SOURCE chunk so the
-// LDS image is the same swz128 image the fragment reads expect (swizzle is an involution).
-// Two stages: the DMA of stage k+1 is in flight while stage k's MFMAs run; one drain + barrier per K-step.
-template <typename TC, int EPI, int BM, int BN>
-__global__ __launch_bounds__(256, 2) void gemm_glds_kernel(GemmArgs g) {
+template <typename TC, int EPI, int BM>
+__global__ __launch_bounds__(256, 1) void gemm_kernel(GemmArgs g) {
+  constexpr int BN = GBN;
   constexpr int E = elems16<TC>();
   constexpr int BKE = 8 * E;
   constexpr int WM = BM / 2, WN = BN / 2;
   constexpr int MT = WM / 16, NT = WN / 16;
   constexpr int AR = BM * 8 / 256, BR = BN * 8 / 256;  // DMA rounds per stage
+  constexpr int DPS = AR + BR;                         // DMA instructions per stage per wave
+  constexpr int NS = 3;                                // LDS stages (2 in flight while one is read)
   typedef typename Slab<TC>::frag frag;
 
-  __shared__ __attribute__((aligned(16))) uint4 lds[2 * (BM + BN) * 8];
-  const int stage_u4 = (BM + BN) * 8;
+  __shared__ __attribute__((aligned(16))) uint4 lds[GemmLds<BM>::bytes / 16];
+  constexpr int stage_u4 = GemmLds<BM>::stage_bytes / 16;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid >> 1, wn = wid & 1;
   const int ntn = (g.N + BN - 1) / BN;
-  const int bid = blockIdx.x;
+  // XCD-aware remap (cdna_hip_programming.md T1, bijective form): blocks b and b+8 share an
+  // XCD, so give each XCD a contiguous run of n-fastest tiles -> its L2 holds whole A panels
+  const int nwg = gridDim.x, b = blockIdx.x, xq = nwg >> 3, xr = nwg & 7, xcd = b & 7;
+  const int bid = (xcd < xr ? xcd * (xq + 1) : xr * (xq + 1) + (xcd - xr) * xq) + (b >> 3);
   const int m0 = (bid / ntn) * BM, n0 = (bid % ntn) * BN;
   const TC* A = reinterpret_cast<const TC*>(g.A);
   const TC* W = reinterpret_cast<const TC*>(g.W);
 
-  // per-lane source offsets (elements), fixed across K-steps
+  // per-lane DMA source offsets (elements), fixed across K-steps. The swizzle goes on the
+  // SOURCE chunk so that (wave-uniform LDS base + lane*16) lands on the swz128 image.
   int64_t aoff[AR], boff[BR];
-#pragma unroll
-  for (int i = 0; i < AR; ++i) {
-    int p = (i * 4 + wid) * 64 + lane, row = p >> 3, slot = p & 7;
-    int m = min(m0 + row, g.M - 1);
+  static_for<0, AR>([&](auto I) {
+    constexpr int i = decltype(I)::value;
+    const int p = (i * 4 + wid) * 64 + lane, row = p >> 3, slot = p & 7;
+    const int m = min(m0 + row, g.M - 1);  // rows past M feed only unstored outputs
     aoff[i] = (int64_t)m * g.lda + swz128(row, slot) * E;
-  }
-#pragma unroll
-  for (int i = 0; i < BR; ++i) {
-    int p = (i * 4 + wid) * 64 + lane, row = p >> 3, slot = p & 7;
+  });
+  static_for<0, BR>([&](auto I) {
+    constexpr int i = decltype(I)::value;
+    const int p = (i * 4 + wid) * 64 + lane, row = p >> 3, slot = p & 7;
     boff[i] = (int64_t)(n0 + row) * g.ldw + swz128(row, slot) * E;
-  }
+  });
   auto stage = [&](int buf, int k0) {
     uint4* As = lds + buf * stage_u4;
     uint4* Bs = As + BM * 8;
-#pragma unroll
-    for (int i = 0; i < AR; ++i)
+    static_for<0, AR>([&](auto I) {
+      constexpr int i = decltype(I)::value;
       __builtin_amdgcn_global_load_lds((const void*)(A + aoff[i] + k0), (LDS_PTR(void))(As + (i * 4 + wid) * 64),
                                        16, 0, 0);
-#pragma unroll
-    for (int i = 0; i < BR; ++i)
+    });
+    static_for<0, BR>([&](auto I) {
+      constexpr int i = decltype(I)::value;
       __builtin_amdgcn_global_load_lds((const void*)(W + boff[i] + k0), (LDS_PTR(void))(Bs + (i * 4 + wid) * 64),
                                        16, 0, 0);
+    });
   };
+
+  // Fragment reads are inline-asm ds_read_b128 so that hipcc does not put a vmcnt(0) (for the
+  // LDS-DMA still in flight into the OTHER stages) in front of them; their completion is waited
+  // for by hand (lgkmcnt(0) + sched_barrier, cdna_hip_programming.md §5.7 form iii).
+  // Row r of a fragment has r & 7 == lane & 7, so the swizzled chunk depends only on the lane:
+  // per slab one base address per lane, the 16-row tiles at immediate offsets i*2048.
+  const uint32_t lds0 = (uint32_t)(uintptr_t)(LDS_PTR(void))lds;
+  const int fr = lane & 15, q = lane >> 4;
+  uint32_t abase[2], bbase[2];
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+    abase[s] = lds0 + (wm * WM + fr) * 128 + swz128(fr, s * 4 + q) * 16;
+    bbase[s] = lds0 + BM * 128 + (wn * WN + fr) * 128 + swz128(fr, s * 4 + q) * 16;
+  }
 
   f32x4 acc[MT][NT];
 #pragma unroll
@@ -141,52 +243,99 @@ __global__ __launch_bounds__(256, 2) void gemm_glds_kernel(GemmArgs g) {
 
   const int nk = g.K / BKE;
   stage(0, 0);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
+  if (nk > 1) stage(1, BKE);
   for (int kt = 0; kt < nk; ++kt) {
-    const int cur = kt & 1;
-    const uint4* As = lds + cur * stage_u4;
-    const uint4* Bs = As + BM * 8;
-    // all fragment reads of this stage BEFORE the next stage's DMA is issued: hipcc would
-    // otherwise wait vmcnt(0) (the pending LDS-DMA) in front of the first ds_read
-    frag af[2][MT], bfr[2][NT];
+    // stage kt has landed for THIS wave once at most the next stage's DMAs are outstanding;
+    // the barrier then publishes every wave's part of it
+    if (kt + 1 < nk)
+      asm volatile("s_waitcnt vmcnt(%0)" ::"i"(DPS) : "memory");
+    else
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    const uint32_t soff = (uint32_t)((kt % NS) * GemmLds<BM>::stage_bytes);
+    u32x4 ar[2][MT], br[2][NT];
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
-      const int ch = s * 4 + (lane >> 4);
-#pragma unroll
-      for (int i = 0; i < MT; ++i) {
-        int row = wm * WM + i * 16 + (lane & 15);
-        uint4 v = As[row * 8 + swz128(row, ch)];
-        af[s][i] = __builtin_bit_cast(frag, v);
-      }
-#pragma unroll
-      for (int j = 0; j < NT; ++j) {
-        int row = wn * WN + j * 16 + (lane & 15);
-        uint4 v = Bs[row * 8 + swz128(row, ch)];
-        bfr[s][j] = __builtin_bit_cast(frag, v);
-      }
+      static_for<0, MT>([&](auto I) {
+        constexpr int i = decltype(I)::value;
+        ar[s][i] = lds_read_b128<i * 2048>(abase[s] + soff);
+      });
+      static_for<0, NT>([&](auto J) {
+        constexpr int j = decltype(J)::value;
+        br[s][j] = lds_read_b128<j * 2048>(bbase[s] + soff);
+      });
     }
-    if (kt + 1 < nk) stage(cur ^ 1, (kt + 1) * BKE);
+    // WAR: stage (kt+2)%3 == (kt-1)%3 was last read in iteration kt-1, whose reads all completed
+    // before that iteration's MFMAs, i.e. before every wave reached this iteration's barrier
+    if (kt + 2 < nk) stage((kt + 2) % NS, (kt + 2) * BKE);
+    // slab 0's reads are the oldest MT+NT LDS ops: consume them while slab 1's land
+    asm volatile("s_waitcnt lgkmcnt(%0)" ::"i"(MT + NT) : "memory");
 #pragma unroll
-    for (int s = 0; s < 2; ++s)
+    for (int i = 0; i < MT; ++i) asm volatile("" : "+v"(ar[0][i]));
 #pragma unroll
-      for (int i = 0; i < MT; ++i)
-#pragma unroll
-        for (int j = 0; j < NT; ++j) acc[i][j] = Slab<TC>::mma(af[s][i], bfr[s][j], acc[i][j]);
-    // keep the MFMAs above the DMA drain (asm "memory" does not order register-only MFMAs)
+    for (int j = 0; j < NT; ++j) asm volatile("" : "+v"(br[0][j]));
     __builtin_amdgcn_sched_barrier(0);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < MT; ++i)
+#pragma unroll
+      for (int j = 0; j < NT; ++j)
+        acc[i][j] = Slab<TC>::mma(__builtin_bit_cast(frag, ar[0][i]), __builtin_bit_cast(frag, br[0][j]), acc[i][j]);
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+    for (int i = 0; i < MT; ++i) asm volatile("" : "+v"(ar[1][i]));
+#pragma unroll
+    for (int j = 0; j < NT; ++j) asm volatile("" : "+v"(br[1][j]));
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int i = 0; i < MT; ++i)
+#pragma unroll
+      for (int j = 0; j < NT; ++j)
+        acc[i][j] = Slab<TC>::mma(__builtin_bit_cast(frag, ar[1][i]), __builtin_bit_cast(frag, br[1][j]), acc[i][j]);
   }
-  epilogue<TC, EPI, BM, BN>(g, acc, m0, n0, wm, wn, lane);
+  __syncthreads();
+
+  // ---- epilogue: accumulators -> LDS (fp32, padded rows) -> row-contiguous 8-column chunks
+  float* Cs = reinterpret_cast<float*>(lds);
+#pragma unroll
+  for (int i = 0; i < MT; ++i)
+#pragma unroll
+    for (int j = 0; j < NT; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        Cs[(wm * WM + i * 16 + (lane >> 4) * 4 + r) * CPAD + wn * WN + j * 16 + (lane & 15)] = acc[i][j][r];
+  __syncthreads();
+  const int cg = tid & 15;  // 16 threads x 8 columns per row
+#pragma unroll 2
+  for (int rr = tid >> 4; rr < BM; rr += 16) {
+    const int row = m0 + rr, col = n0 + cg * 8;
+    if (row >= g.M || col >= g.N) continue;
+    const float* src = Cs + rr * CPAD + cg * 8;
+    float4 a = *reinterpret_cast<const float4*>(src), b = *reinterpret_cast<const float4*>(src + 4);
+    epi8<TC, EPI>(g, row, col, V8{{a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w}});
+  }
+}
+
+static int gemm_bm_override() {
+  static int v = [] {
+    const char* e = getenv("F5H_GEMM_BM");  // tuning experiments only: 64 or 128
+    return e ? atoi(e) : 0;
+  }();
+  return v;
 }
 
 template <typename TC, int EPI>
 static hipError_t launch_t(const GemmArgs& a, hipStream_t st) {
-  constexpr int BM = 128, BN = 128;
-  const int grid = ((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN);
-  if (grid == 0) return hipSuccess;
-  hipLaunchKernelGGL((gemm_glds_kernel<TC, EPI, BM, BN>), dim3(grid), dim3(256), 0, st, a);
+  const int ntn = (a.N + GBN - 1) / GBN;
+  const int t128 = ((a.M + 127) / 128) * ntn;
+  if (t128 == 0) return hipSuccess;
+  const int ov = gemm_bm_override();
+  if (ov == 128 || (ov == 0 && t128 >= 1024)) {  // enough 128-row tiles for >= 4 per CU
+    hipLaunchKernelGGL((gemm_kernel<TC, EPI, 128>), dim3(t128), dim3(256), 0, st, a);
+  } else {
+    const int t64 = ((a.M + 63) / 64) * ntn;
+    hipLaunchKernelGGL((gemm_kernel<TC, EPI, 64>), dim3(t64), dim3(256), 0, st, a);
+  }
   return hipGetLastError();
 }
 
@@ -208,6 +357,9 @@ static hipError_t launch_epi(int epi, const GemmArgs& a, hipStream_t st) {
 hipError_t gemm(int compute, int epi, const GemmArgs& a, hipStream_t st) {
   const int bke = compute ? 64 : 32;
   if (a.K % bke != 0 || a.M < 0 || a.N <= 0 || a.lda % 8 || a.ldw % 8) return hipErrorInvalidValue;
+  // 8-column epilogue chunks: vector paths need 16 B alignment of every operand row
+  if (epi == EPI_INPROJ && (a.ldc % 8 || a.ld_add % 8 || a.N % 8)) return hipErrorInvalidValue;
+  if (epi == EPI_QKV && (a.N % 64)) return hipErrorInvalidValue;
   return compute ? launch_epi<bf16>(epi, a, st) : launch_epi<float>(epi, a, st);
 }
 

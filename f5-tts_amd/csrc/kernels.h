@@ -31,6 +31,7 @@ struct GemmArgs {
   int seq_len;                     // L: rows per sequence
   int heads, rope_heads;
   void* q; void* k; void* v;
+  float q_scale;                   // EPI_QKV: q is stored pre-multiplied by this (0 -> 1)
 };
 
 // compute: 0 fp32 operands, 1 bf16 operands. A and W both in the operand dtype.
@@ -42,6 +43,7 @@ struct AttnArgs {
   int S, H, L;
   const int32_t* kv_len;  // [S] or null
   float scale;            // 1/sqrt(64)
+  int prescaled;          // q already carries scale*log2(e): scores are in log2 units
 };
 hipError_t attention(int compute, const AttnArgs& a, hipStream_t st);
 
@@ -84,7 +86,7 @@ hipError_t dwconv_ln(int compute, const float* x, int S, int L, int C, const flo
                      const float* ln_w, const float* ln_b, void* out, hipStream_t st);
 // GRN: sumsq[s,c] = sum_n x^2 ; then out = gamma*(x*Nx)+beta+x -> operand dtype
 hipError_t grn(int compute, const float* x, int S, int L, int C, const float* gamma, const float* beta,
-               float* scratch /*[S*C + S]*/, void* out, hipStream_t st);
+               float* scratch /*[(ceil(L/64)+1)*S*C]*/, void* out, hipStream_t st);
 // A_ct [S*N, 128 + td] operand dtype: [where(cond_mask,cond,0) (zeros for uncond) pad 128 | text]
 hipError_t build_ct(int compute, const float* cond, const uint8_t* cond_mask, const float* text_c,
                     const float* text_u, int B, int N, int td, int S, void* out, hipStream_t st);
