@@ -224,7 +224,8 @@ __global__ __launch_bounds__(256, 1) void gemm_kernel(GemmArgs g) {
   // Fragment reads are inline-asm ds_read_b128 so that hipcc does not put a vmcnt(0) (for the
   // LDS-DMA still in flight into the OTHER stages) in front of them; their completion is waited
   // for by hand (lgkmcnt(0) + sched_barrier, cdna_hip_programming.md §5.7 form iii).
-  // Row r of a fragment has r & 7 == lane & 7, so the swizzled chunk depends only on the lane:
+  // Row r of a fragment has r & 15 == lane & 15 (swz128 reads row bits 1..3), so the swizzled
+  // chunk depends only on the lane:
   // per slab one base address per lane, the 16-row tiles at immediate offsets i*2048.
   const uint32_t lds0 = (uint32_t)(uintptr_t)(LDS_PTR(void))lds;
   const int fr = lane & 15, q = lane >> 4;
