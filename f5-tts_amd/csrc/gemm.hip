@@ -25,10 +25,10 @@ namespace f5h {
 constexpr int GBN = 128;         // block tile columns
 constexpr int CPAD = GBN + 4;    // fp32 epilogue staging row (528 B: conflict-free MFMA-layout writes)
 
-template <int BM>
+template <int BM, int NS>
 struct GemmLds {
   static constexpr int stage_bytes = (BM + GBN) * 128;
-  static constexpr int main_bytes = 3 * stage_bytes;
+  static constexpr int main_bytes = NS * stage_bytes;
   static constexpr int epi_bytes = BM * CPAD * 4;
   static constexpr int bytes = main_bytes > epi_bytes ? main_bytes : epi_bytes;
 };
@@ -167,7 +167,18 @@ F5H_DEV void epi8(const GemmArgs& g, int row, int col, V8 x) {
   }
 }
 
-template <typename TC, int EPI, int BM>
+// wait until at most `n` of this wave's VMEM ops (n/DPS stages) are outstanding
+template <int DPS>
+F5H_DEV void wait_stages(int n_stages) {
+  switch (n_stages) {
+    case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+    case 1: asm volatile("s_waitcnt vmcnt(%0)" ::"i"(DPS) : "memory"); break;
+    case 2: asm volatile("s_waitcnt vmcnt(%0)" ::"i"(2 * DPS) : "memory"); break;
+    default: asm volatile("s_waitcnt vmcnt(%0)" ::"i"(3 * DPS) : "memory"); break;
+  }
+}
+
+template <typename TC, int EPI, int BM, int NS>
 __global__ __launch_bounds__(256, 1) void gemm_kernel(GemmArgs g) {
   constexpr int BN = GBN;
   constexpr int E = elems16<TC>();
@@ -176,11 +187,11 @@ __global__ __launch_bounds__(256, 1) void gemm_kernel(GemmArgs g) {
   constexpr int MT = WM / 16, NT = WN / 16;
   constexpr int AR = BM * 8 / 256, BR = BN * 8 / 256;  // DMA rounds per stage
   constexpr int DPS = AR + BR;                         // DMA instructions per stage per wave
-  constexpr int NS = 3;                                // LDS stages (2 in flight while one is read)
+  static_assert(NS >= 2 && NS <= 5, "LDS stages");  // NS-1 stages in flight while one is read
   typedef typename Slab<TC>::frag frag;
 
-  __shared__ __attribute__((aligned(16))) uint4 lds[GemmLds<BM>::bytes / 16];
-  constexpr int stage_u4 = GemmLds<BM>::stage_bytes / 16;
+  __shared__ __attribute__((aligned(16))) uint4 lds[GemmLds<BM, NS>::bytes / 16];
+  constexpr int stage_u4 = GemmLds<BM, NS>::stage_bytes / 16;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid >> 1, wn = wid & 1;
   const int ntn = (g.N + BN - 1) / BN;
@@ -243,17 +254,13 @@ __global__ __launch_bounds__(256, 1) void gemm_kernel(GemmArgs g) {
     for (int j = 0; j < NT; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   const int nk = g.K / BKE;
-  stage(0, 0);
-  if (nk > 1) stage(1, BKE);
+  for (int p = 0; p < NS - 1 && p < nk; ++p) stage(p, p * BKE);
   for (int kt = 0; kt < nk; ++kt) {
-    // stage kt has landed for THIS wave once at most the next stage's DMAs are outstanding;
+    // stage kt has landed for THIS wave once at most the younger in-flight stages remain;
     // the barrier then publishes every wave's part of it
-    if (kt + 1 < nk)
-      asm volatile("s_waitcnt vmcnt(%0)" ::"i"(DPS) : "memory");
-    else
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    wait_stages<DPS>(min(NS - 2, nk - 1 - kt));
     __builtin_amdgcn_s_barrier();
-    const uint32_t soff = (uint32_t)((kt % NS) * GemmLds<BM>::stage_bytes);
+    const uint32_t soff = (uint32_t)((kt % NS) * GemmLds<BM, NS>::stage_bytes);
     u32x4 ar[2][MT], br[2][NT];
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
@@ -266,9 +273,9 @@ __global__ __launch_bounds__(256, 1) void gemm_kernel(GemmArgs g) {
         br[s][j] = lds_read_b128<j * 2048>(bbase[s] + soff);
       });
     }
-    // WAR: stage (kt+2)%3 == (kt-1)%3 was last read in iteration kt-1, whose reads all completed
-    // before that iteration's MFMAs, i.e. before every wave reached this iteration's barrier
-    if (kt + 2 < nk) stage((kt + 2) % NS, (kt + 2) * BKE);
+    // WAR: slot (kt+NS-1)%NS == (kt-1)%NS was last read in iteration kt-1, whose reads all
+    // completed before that iteration's MFMAs, i.e. before every wave reached this barrier
+    if (kt + NS - 1 < nk) stage((kt + NS - 1) % NS, (kt + NS - 1) * BKE);
     // slab 0's reads are the oldest MT+NT LDS ops: consume them while slab 1's land
     asm volatile("s_waitcnt lgkmcnt(%0)" ::"i"(MT + NT) : "memory");
 #pragma unroll
@@ -317,10 +324,12 @@ __global__ __launch_bounds__(256, 1) void gemm_kernel(GemmArgs g) {
   }
 }
 
-static int gemm_bm_override() {
+// Tile variant: 0 = 64x128 / 3 stages (default), 1 = 128x128 / 2 stages (2 blocks per CU),
+// 2 = 64x128 / 4 stages, 3 = 128x128 / 3 stages. F5H_GEMM_VARIANT overrides (tuning only).
+static int gemm_variant_override() {
   static int v = [] {
-    const char* e = getenv("F5H_GEMM_BM");  // tuning experiments only: 64 or 128
-    return e ? atoi(e) : 0;
+    const char* e = getenv("F5H_GEMM_VARIANT");
+    return e ? atoi(e) : -1;
   }();
   return v;
 }
@@ -328,14 +337,15 @@ static int gemm_bm_override() {
 template <typename TC, int EPI>
 static hipError_t launch_t(const GemmArgs& a, hipStream_t st) {
   const int ntn = (a.N + GBN - 1) / GBN;
-  const int t128 = ((a.M + 127) / 128) * ntn;
+  const int t128 = ((a.M + 127) / 128) * ntn, t64 = ((a.M + 63) / 64) * ntn;
   if (t128 == 0) return hipSuccess;
-  const int ov = gemm_bm_override();
-  if (ov == 128 || (ov == 0 && t128 >= 1024)) {  // enough 128-row tiles for >= 4 per CU
-    hipLaunchKernelGGL((gemm_kernel<TC, EPI, 128>), dim3(t128), dim3(256), 0, st, a);
-  } else {
-    const int t64 = ((a.M + 63) / 64) * ntn;
-    hipLaunchKernelGGL((gemm_kernel<TC, EPI, 64>), dim3(t64), dim3(256), 0, st, a);
+  int v = gemm_variant_override();
+  if (v < 0) v = 0;
+  switch (v) {
+    case 1: hipLaunchKernelGGL((gemm_kernel<TC, EPI, 128, 2>), dim3(t128), dim3(256), 0, st, a); break;
+    case 2: hipLaunchKernelGGL((gemm_kernel<TC, EPI, 64, 4>), dim3(t64), dim3(256), 0, st, a); break;
+    case 3: hipLaunchKernelGGL((gemm_kernel<TC, EPI, 128, 3>), dim3(t128), dim3(256), 0, st, a); break;
+    default: hipLaunchKernelGGL((gemm_kernel<TC, EPI, 64, 3>), dim3(t64), dim3(256), 0, st, a); break;
   }
   return hipGetLastError();
 }

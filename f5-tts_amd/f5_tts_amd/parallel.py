@@ -1,0 +1,77 @@
+"""Data-parallel sharding of utterances over GPUs.
+
+The sampling path never communicates inside the ODE: each rank runs the engine on its own
+utterances. This module holds the two host-side pieces around that:
+
+* `shard_lpt`: longest-processing-time assignment of utterances to ranks by the cost model
+  S*F(N) with F(N) = a*N + b*N^2, the MI355X replacement for the reference's
+  `split_between_processes` (eval_infer_batch.py:181) / `DistributedSampler`
+  (benchmark.py:340-341), which split by count and ignore the quadratic attention term.
+* `gather_mels`: the only collective on the path — an all-gather of per-rank counts and
+  lengths, then of the finished mels (padded to the max per rank), over RCCL (backend
+  "nccl") on GPUs or gloo on CPU.
+"""
+
+from __future__ import annotations
+
+import heapq
+
+import torch
+import torch.distributed as dist
+
+# Base DiT: FLOPs per sequence-forward = A*N + B*N^2
+COST_A, COST_B = 378.888e6, 90112.0
+
+
+def utterance_cost(n_frames: int) -> float:
+    return COST_A * n_frames + COST_B * n_frames * n_frames
+
+
+def shard_lpt(frames, world: int):
+    """Assign utterance indices to `world` ranks, heaviest first onto the least-loaded rank.
+    Returns a list (per rank) of index lists, each sorted by length (for length bucketing)."""
+    order = sorted(range(len(frames)), key=lambda i: -utterance_cost(frames[i]))
+    heap = [(0.0, r) for r in range(world)]
+    out = [[] for _ in range(world)]
+    for i in order:
+        load, r = heapq.heappop(heap)
+        out[r].append(i)
+        heapq.heappush(heap, (load + utterance_cost(frames[i]), r))
+    return [sorted(o, key=lambda i: frames[i]) for o in out]
+
+
+def bucket(indices, frames, max_batch: int):
+    """Split a rank's (length-sorted) utterances into batches of at most `max_batch`
+    (neighbours in length -> little padding, as get_inference_prompt's buckets do)."""
+    idx = sorted(indices, key=lambda i: frames[i])
+    return [idx[k:k + max_batch] for k in range(0, len(idx), max_batch)]
+
+
+def gather_mels(local: "dict[int, torch.Tensor]", device=None, group=None):
+    """All-gather finished mels {utt_index: [n_i, C]} from every rank.
+    Returns {utt_index: tensor} with every utterance of the job (on every rank)."""
+    world = dist.get_world_size(group)
+    dev = device if device is not None else (next(iter(local.values())).device if local else torch.device("cpu"))
+    C = next(iter(local.values())).shape[-1] if local else 100
+    keys = sorted(local)
+    cnt = torch.tensor([len(keys), max([local[k].shape[0] for k in keys], default=0)], dtype=torch.int64, device=dev)
+    cnts = [torch.zeros_like(cnt) for _ in range(world)]
+    dist.all_gather(cnts, cnt, group=group)
+    maxn = max(int(c[0]) for c in cnts)
+    maxl = max(int(c[1]) for c in cnts)
+    meta = torch.full((maxn, 2), -1, dtype=torch.int64, device=dev)
+    buf = torch.zeros(maxn, maxl, C, dtype=torch.float32, device=dev)
+    for j, k in enumerate(keys):
+        meta[j, 0], meta[j, 1] = k, local[k].shape[0]
+        buf[j, : local[k].shape[0]] = local[k].float()
+    metas = [torch.empty_like(meta) for _ in range(world)]
+    bufs = [torch.empty_like(buf) for _ in range(world)]
+    dist.all_gather(metas, meta, group=group)
+    dist.all_gather(bufs, buf, group=group)
+    out = {}
+    for m, b in zip(metas, bufs):
+        for j in range(maxn):
+            k, n = int(m[j, 0]), int(m[j, 1])
+            if k >= 0:
+                out[k] = b[j, :n].clone()
+    return out

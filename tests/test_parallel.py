@@ -1,0 +1,68 @@
+"""Multi-process (gloo, world_size 2) coverage of the data-parallel path: LPT sharding, length
+bucketing and the all-gather of finished mels (the only collective on the sampling path)."""
+
+import os
+import socket
+
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from f5_tts_amd import parallel, synthetic
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def test_lpt_balances_quadratic_cost():
+    c3 = synthetic.c3_case()
+    frames = c3["total"]
+    shards = parallel.shard_lpt(frames, 8)
+    assert sorted(i for s in shards for i in s) == list(range(len(frames)))
+    loads = [sum(parallel.utterance_cost(frames[i]) for i in s) for s in shards]
+    assert max(loads) / min(loads) < 1.15
+    # count-based split (what split_between_processes does) is worse for ragged lengths
+    naive = [list(range(r * 4, r * 4 + 4)) for r in range(8)]
+    nl = [sum(parallel.utterance_cost(frames[i]) for i in s) for s in naive]
+    assert max(loads) < max(nl)
+
+
+def test_bucket_keeps_neighbours():
+    frames = [100, 900, 300, 500, 700, 200]
+    b = parallel.bucket(range(6), frames, 2)
+    assert [[frames[i] for i in x] for x in b] == [[100, 200], [300, 500], [700, 900]]
+
+
+def _worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    frames = [120, 80, 200, 50, 160]
+    shards = parallel.shard_lpt(frames, world)
+    # stand-in for the engine's output: a deterministic mel per utterance
+    local = {i: torch.full((frames[i], 100), float(i)) + torch.arange(frames[i])[:, None] for i in shards[rank]}
+    got = parallel.gather_mels(local)
+    ok = sorted(got) == list(range(len(frames))) and all(
+        torch.equal(got[i], torch.full((frames[i], 100), float(i)) + torch.arange(frames[i])[:, None])
+        for i in range(len(frames)))
+    q.put((rank, ok, [len(s) for s in shards]))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_gather_mels_world2_gloo():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+    assert all(ok for _, ok, _ in res), res
+    assert all(p.exitcode == 0 for p in procs)
