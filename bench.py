@@ -73,6 +73,14 @@ def cpu_baseline(case, arch, threads):
             "rtf": full / (gen * HOP / SR)}
 
 
+def class_flops(kc, arch, S, L):
+    """Algorithmic FLOPs of one launch of a probed kernel class (SURVEY §8d per-op terms)."""
+    d, ff = arch["dim"], int(arch["dim"] * arch["ff_mult"])
+    return {"attention": attn_flops(S, arch["heads"], L), "ffn1": 2.0 * S * L * d * ff, "ffn2": 2.0 * S * L * d * ff,
+            "qkv": 2.0 * S * L * d * 3 * d, "out": 2.0 * S * L * d * d,
+            "conv": 2.0 * S * L * d * (d // 16) * 31}.get(kc, 0.0)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -82,6 +90,8 @@ def main():
     ap.add_argument("--compute", default="bf16")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--probe", default="attention", help="kernel class timed with HIP events for the roofline")
+    ap.add_argument("--probe-all", action="store_true",
+                    help="after the measurement, time every kernel class in its own loop (table on stderr)")
     args = ap.parse_args()
 
     from f5_tts_amd import synthetic
@@ -145,18 +155,26 @@ def main():
     roof = None
     if n_launch:
         avg_ms = probe_ms / n_launch
-        if args.probe == "attention":
-            fl = attn_flops(S, H, L)
-        elif args.probe in ("ffn1", "ffn2"):
-            fl = 2.0 * S * L * arch["dim"] * int(arch["dim"] * arch["ff_mult"])
-        elif args.probe == "qkv":
-            fl = 2.0 * S * L * arch["dim"] * 3 * arch["dim"]
-        else:
-            fl = 2.0 * S * L * arch["dim"] * (arch["dim"] // 16) * 31
-        ach = fl / (avg_ms * 1e-3) / 1e12
+        fl = class_flops(args.probe, arch, S, L)
+        ach = fl / (avg_ms * 1e-3) / 1e12 if fl else 0.0
         roof = {"bound": "mfma", "kernel": args.probe, "achieved": round(ach, 2), "peak": PEAK_BF16_TFLOPS,
                 "unit": "TFLOP/s", "frac": round(ach / PEAK_BF16_TFLOPS, 4), "traffic": None,
                 "avg_launch_ms": round(avg_ms, 5), "launches": n_launch, "flops_per_launch": fl}
+
+    if args.probe_all and rank == 0:
+        import sys
+        for kc in ("qkv", "attention", "out", "norm", "ffn1", "ffn2", "conv"):
+            eng.probe(kc)
+            for _ in range(max(1, min(args.steps, 3))):
+                step()
+            torch.cuda.synchronize()
+            n, ms = eng.probe_read()
+            eng.probe(None)
+            if n:
+                avg = ms / n
+                fl = class_flops(kc, arch, S, L)
+                print(f"[probe] {kc:9s} launches/call {n // max(1, min(args.steps, 3)):4d}  avg {avg * 1e3:8.2f} us"
+                      + (f"  {fl / (avg * 1e-3) / 1e12:7.1f} TF/s" if fl else ""), file=sys.stderr, flush=True)
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

@@ -393,7 +393,7 @@ static void layout(const f5h_engine* e, WS& ws, Bufs& b, int B, int N, int nfe, 
 }
 
 // ---------------------------------------------------------------- probe
-enum { KC_FFN1 = 0, KC_ATTN = 1, KC_QKV = 2, KC_FFN2 = 3, KC_CONV = 4 };
+enum { KC_FFN1 = 0, KC_ATTN = 1, KC_QKV = 2, KC_FFN2 = 3, KC_CONV = 4, KC_OUT = 5, KC_NORM = 6 };
 struct ProbeScope {
   f5h_engine* e;
   hipStream_t st;
@@ -619,12 +619,16 @@ static int backbone_step(Ctx& c, int k) {
       GemmArgs g = gargs(b.o, inner, Ly.out, rows, h, d);
       g.gate = ad ? ad + 2 * d : nullptr;  // gate_msa
       g.rowkeep = keep;                    // masked_fill of pad rows (modules.py:552-554)
+      ProbeScope ps(e, KC_OUT, st);
       KCK(gemm(bf, EPI_RESID, g, st));
     }
-    if (dit)
-      KCK(ln_modulate(bf, h, rows, d, ad + 3 * d /*shift_mlp*/, ad + 4 * d /*scale_mlp*/, b.aop, st));
-    else
-      KCK(rms_norm_g(bf, h, rows, d, Ly.g_ff, b.aop, st));
+    {
+      ProbeScope ps(e, KC_NORM, st);
+      if (dit)
+        KCK(ln_modulate(bf, h, rows, d, ad + 3 * d /*shift_mlp*/, ad + 4 * d /*scale_mlp*/, b.aop, st));
+      else
+        KCK(rms_norm_g(bf, h, rows, d, Ly.g_ff, b.aop, st));
+    }
     {
       GemmArgs g = gargs(b.aop, d, Ly.ff1, rows, b.f, a.ff_dim);
       ProbeScope ps(e, KC_FFN1, st);
@@ -850,6 +854,12 @@ int f5h_op_linear(void* stream, int32_t compute, int32_t M, int32_t N, int32_t K
   g.C = C;
   g.ldc = N;
   HIPCK(gemm(compute, EPI_STORE, g, st));
+  return 0;
+}
+
+int f5h_gemm_force_config(int32_t cfg) {
+  if (cfg < -1 || cfg > 7) return fail(F5H_EINVAL, "gemm config must be -1..7");
+  gemm_force_config(cfg);
   return 0;
 }
 

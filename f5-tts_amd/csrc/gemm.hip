@@ -22,15 +22,18 @@
 
 namespace f5h {
 
-constexpr int GBN = 128;         // block tile columns
-constexpr int CPAD = GBN + 4;    // fp32 epilogue staging row (528 B: conflict-free MFMA-layout writes)
-
-template <int BM, int NS>
-struct GemmLds {
-  static constexpr int stage_bytes = (BM + GBN) * 128;
+// Block tile BM x BN with WGM x WGN waves; every wave owns a (BM/WGM) x (BN/WGN) sub-tile.
+template <int BM, int BN, int WGM, int WGN, int NS>
+struct GemmCfg {
+  static constexpr int NW = WGM * WGN, THREADS = 64 * NW;
+  static constexpr int WM = BM / WGM, WN = BN / WGN, MT = WM / 16, NT = WN / 16;
+  static constexpr int stage_bytes = (BM + BN) * 128;
   static constexpr int main_bytes = NS * stage_bytes;
-  static constexpr int epi_bytes = BM * CPAD * 4;
+  static constexpr int EPAD = WN + 4;                        // fp32 row of a wave's epilogue strip
+  static constexpr int epi_bytes = NW * 16 * EPAD * 4;       // one 16-row strip per wave
   static constexpr int bytes = main_bytes > epi_bytes ? main_bytes : epi_bytes;
+  static_assert(BM * 8 % THREADS == 0 && BN * 8 % THREADS == 0, "whole DMA rounds per stage");
+  static_assert(MT * 16 == WM && NT * 16 == WN && MT + NT <= 15, "fragment counts (lgkmcnt <= 15)");
 };
 
 // ds_read_b128 the compiler does not see (no waitcnt bookkeeping): the caller waits lgkmcnt itself
@@ -178,22 +181,21 @@ F5H_DEV void wait_stages(int n_stages) {
   }
 }
 
-template <typename TC, int EPI, int BM, int NS>
-__global__ __launch_bounds__(256, 1) void gemm_kernel(GemmArgs g) {
-  constexpr int BN = GBN;
+template <typename TC, int EPI, int BM, int BN, int WGM, int WGN, int NS>
+__global__ __launch_bounds__(64 * WGM * WGN, 1) void gemm_kernel(GemmArgs g) {
+  typedef GemmCfg<BM, BN, WGM, WGN, NS> C;
   constexpr int E = elems16<TC>();
   constexpr int BKE = 8 * E;
-  constexpr int WM = BM / 2, WN = BN / 2;
-  constexpr int MT = WM / 16, NT = WN / 16;
-  constexpr int AR = BM * 8 / 256, BR = BN * 8 / 256;  // DMA rounds per stage
-  constexpr int DPS = AR + BR;                         // DMA instructions per stage per wave
-  static_assert(NS >= 2 && NS <= 5, "LDS stages");  // NS-1 stages in flight while one is read
+  constexpr int NW = C::NW, WM = C::WM, WN = C::WN, MT = C::MT, NT = C::NT;
+  constexpr int AR = BM * 8 / C::THREADS, BR = BN * 8 / C::THREADS;  // DMA rounds per stage
+  constexpr int DPS = AR + BR;                                        // DMA instructions per stage per wave
+  static_assert(NS >= 2 && NS <= 4, "LDS stages");  // NS-1 stages in flight while one is read
   typedef typename Slab<TC>::frag frag;
 
-  __shared__ __attribute__((aligned(16))) uint4 lds[GemmLds<BM, NS>::bytes / 16];
-  constexpr int stage_u4 = GemmLds<BM, NS>::stage_bytes / 16;
+  __shared__ __attribute__((aligned(16))) uint4 lds[C::bytes / 16];
+  constexpr int stage_u4 = C::stage_bytes / 16;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int wm = wid >> 1, wn = wid & 1;
+  const int wm = wid / WGN, wn = wid % WGN;
   const int ntn = (g.N + BN - 1) / BN;
   // XCD-aware remap (cdna_hip_programming.md T1, bijective form): blocks b and b+8 share an
   // XCD, so give each XCD a contiguous run of n-fastest tiles -> its L2 holds whole A panels
@@ -208,26 +210,27 @@ __global__ __launch_bounds__(256, 1) void gemm_kernel(GemmArgs g) {
   int64_t aoff[AR], boff[BR];
   static_for<0, AR>([&](auto I) {
     constexpr int i = decltype(I)::value;
-    const int p = (i * 4 + wid) * 64 + lane, row = p >> 3, slot = p & 7;
+    const int p = (i * NW + wid) * 64 + lane, row = p >> 3, slot = p & 7;
     const int m = min(m0 + row, g.M - 1);  // rows past M feed only unstored outputs
     aoff[i] = (int64_t)m * g.lda + swz128(row, slot) * E;
   });
   static_for<0, BR>([&](auto I) {
     constexpr int i = decltype(I)::value;
-    const int p = (i * 4 + wid) * 64 + lane, row = p >> 3, slot = p & 7;
-    boff[i] = (int64_t)(n0 + row) * g.ldw + swz128(row, slot) * E;
+    const int p = (i * NW + wid) * 64 + lane, row = p >> 3, slot = p & 7;
+    const int n = min(n0 + row, g.N - 1);  // likewise for weight rows past N
+    boff[i] = (int64_t)n * g.ldw + swz128(row, slot) * E;
   });
   auto stage = [&](int buf, int k0) {
     uint4* As = lds + buf * stage_u4;
     uint4* Bs = As + BM * 8;
     static_for<0, AR>([&](auto I) {
       constexpr int i = decltype(I)::value;
-      __builtin_amdgcn_global_load_lds((const void*)(A + aoff[i] + k0), (LDS_PTR(void))(As + (i * 4 + wid) * 64),
+      __builtin_amdgcn_global_load_lds((const void*)(A + aoff[i] + k0), (LDS_PTR(void))(As + (i * NW + wid) * 64),
                                        16, 0, 0);
     });
     static_for<0, BR>([&](auto I) {
       constexpr int i = decltype(I)::value;
-      __builtin_amdgcn_global_load_lds((const void*)(W + boff[i] + k0), (LDS_PTR(void))(Bs + (i * 4 + wid) * 64),
+      __builtin_amdgcn_global_load_lds((const void*)(W + boff[i] + k0), (LDS_PTR(void))(Bs + (i * NW + wid) * 64),
                                        16, 0, 0);
     });
   };
@@ -260,7 +263,7 @@ __global__ __launch_bounds__(256, 1) void gemm_kernel(GemmArgs g) {
     // the barrier then publishes every wave's part of it
     wait_stages<DPS>(min(NS - 2, nk - 1 - kt));
     __builtin_amdgcn_s_barrier();
-    const uint32_t soff = (uint32_t)((kt % NS) * GemmLds<BM, NS>::stage_bytes);
+    const uint32_t soff = (uint32_t)((kt % NS) * C::stage_bytes);
     u32x4 ar[2][MT], br[2][NT];
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
@@ -303,49 +306,94 @@ __global__ __launch_bounds__(256, 1) void gemm_kernel(GemmArgs g) {
   }
   __syncthreads();
 
-  // ---- epilogue: accumulators -> LDS (fp32, padded rows) -> row-contiguous 8-column chunks
-  float* Cs = reinterpret_cast<float*>(lds);
+  // ---- epilogue, per wave and 16-row strip: accumulators -> the wave's LDS strip (fp32,
+  // padded rows) -> 8-column chunks of whole rows, so the epilogue's global accesses are
+  // 16-32 B vectors along rows. Strips are wave-private: LDS order within a wave suffices.
+  float* Cs = reinterpret_cast<float*>(lds) + wid * 16 * C::EPAD;
+  constexpr int CH = WN / 8;  // 8-column chunks per strip row
 #pragma unroll
-  for (int i = 0; i < MT; ++i)
+  for (int i = 0; i < MT; ++i) {
 #pragma unroll
     for (int j = 0; j < NT; ++j)
 #pragma unroll
-      for (int r = 0; r < 4; ++r)
-        Cs[(wm * WM + i * 16 + (lane >> 4) * 4 + r) * CPAD + wn * WN + j * 16 + (lane & 15)] = acc[i][j][r];
-  __syncthreads();
-  const int cg = tid & 15;  // 16 threads x 8 columns per row
-#pragma unroll 2
-  for (int rr = tid >> 4; rr < BM; rr += 16) {
-    const int row = m0 + rr, col = n0 + cg * 8;
-    if (row >= g.M || col >= g.N) continue;
-    const float* src = Cs + rr * CPAD + cg * 8;
-    float4 a = *reinterpret_cast<const float4*>(src), b = *reinterpret_cast<const float4*>(src + 4);
-    epi8<TC, EPI>(g, row, col, V8{{a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w}});
+      for (int r = 0; r < 4; ++r) Cs[(q * 4 + r) * C::EPAD + j * 16 + fr] = acc[i][j][r];
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+    for (int t = 0; t < 16 * CH / 64; ++t) {
+      const int idx = t * 64 + lane, rr = idx / CH, cc = idx % CH;
+      const int row = m0 + wm * WM + i * 16 + rr, col = n0 + wn * WN + cc * 8;
+      const float* src = Cs + rr * C::EPAD + cc * 8;
+      float4 a = *reinterpret_cast<const float4*>(src), b = *reinterpret_cast<const float4*>(src + 4);
+      if (row < g.M && col < g.N) epi8<TC, EPI>(g, row, col, V8{{a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w}});
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   }
 }
 
-// Tile variant: 0 = 64x128 / 3 stages (default), 1 = 128x128 / 2 stages (2 blocks per CU),
-// 2 = 64x128 / 4 stages, 3 = 128x128 / 3 stages. F5H_GEMM_VARIANT overrides (tuning only).
-static int gemm_variant_override() {
+// Tile configurations (bf16; the fp32 parity mode always uses cfg 0):
+//   0: 64x128,  4 waves (2x2, 32x64 each),  3 stages, 2 blocks/CU
+//   1: 128x128, 4 waves (2x2, 64x64 each),  2 stages, 2 blocks/CU
+//   2: 128x256, 8 waves (2x4, 64x64 each),  3 stages, 1 block/CU
+//   3: 192x256, 8 waves (2x4, 96x64 each),  2 stages, 1 block/CU
+//   4: 256x128, 8 waves (4x2, 64x64 each),  3 stages, 1 block/CU
+//   5: 192x128, 4 waves (2x2, 96x64 each),  2 stages, 2 blocks/CU
+//   6: 128x128, 8 waves (4x2, 32x64 each),  3 stages, 1 block/CU
+//   7: 256x256, 8 waves (2x4, 128x64 each), 2 stages, 1 block/CU
+// Per-CU LDS-DMA intake (~37 B/clk) bounds the small tiles: bytes per MFLOP staged =
+// 64*(BM+BN)/(BM*BN) KB, so 64x128 -> 24, 128x256 -> 12, 192x256 -> 9.3.
+static int g_force_cfg = -1;
+static int gemm_env_cfg() {
   static int v = [] {
-    const char* e = getenv("F5H_GEMM_VARIANT");
+    const char* e = getenv("F5H_GEMM_CFG");
     return e ? atoi(e) : -1;
   }();
   return v;
 }
 
+template <typename TC, int EPI, int BM, int BN, int WGM, int WGN, int NS>
+static void launch_cfg(const GemmArgs& a, hipStream_t st) {
+  const int tiles = ((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN);
+  hipLaunchKernelGGL((gemm_kernel<TC, EPI, BM, BN, WGM, WGN, NS>), dim3(tiles), dim3(64 * WGM * WGN), 0, st, a);
+}
+
+// Tile choice for a bf16 GEMM among the 2-blocks-per-CU configurations 0, 1, 5: time ~
+// rounds x tile work / relative efficiency, with rounds = ceil(tiles / 512 block slots) and
+// efficiencies from tools/gemm_tune.py on MI355X (C3-sized GEMMs: 64x128 0.57, 128x128 0.74,
+// 192x128 0.86 of the best). C2 picks 192x128 for QKV, 128x128 for FFN1, 64x128 for N = 1024.
+static int pick_cfg(const GemmArgs& a) {
+  struct Opt { int cfg, bm, bn; float eff; };
+  constexpr Opt opts[3] = {{5, 192, 128, 0.86f}, {1, 128, 128, 0.74f}, {0, 64, 128, 0.57f}};
+  int best = 0;
+  double tbest = 1e300;
+  for (const Opt& o : opts) {
+    const int64_t tiles = (int64_t)((a.M + o.bm - 1) / o.bm) * ((a.N + o.bn - 1) / o.bn);
+    const double t = (double)((tiles + 511) / 512) * o.bm * o.bn / o.eff;
+    if (t < tbest * 0.999) tbest = t, best = o.cfg;
+  }
+  return best;
+}
+
 template <typename TC, int EPI>
 static hipError_t launch_t(const GemmArgs& a, hipStream_t st) {
-  const int ntn = (a.N + GBN - 1) / GBN;
-  const int t128 = ((a.M + 127) / 128) * ntn, t64 = ((a.M + 63) / 64) * ntn;
-  if (t128 == 0) return hipSuccess;
-  int v = gemm_variant_override();
-  if (v < 0) v = 0;
-  switch (v) {
-    case 1: hipLaunchKernelGGL((gemm_kernel<TC, EPI, 128, 2>), dim3(t128), dim3(256), 0, st, a); break;
-    case 2: hipLaunchKernelGGL((gemm_kernel<TC, EPI, 64, 4>), dim3(t64), dim3(256), 0, st, a); break;
-    case 3: hipLaunchKernelGGL((gemm_kernel<TC, EPI, 128, 3>), dim3(t128), dim3(256), 0, st, a); break;
-    default: hipLaunchKernelGGL((gemm_kernel<TC, EPI, 64, 3>), dim3(t64), dim3(256), 0, st, a); break;
+  if (a.M == 0) return hipSuccess;
+  int cfg = 0;
+  if constexpr (std::is_same<TC, bf16>::value) {
+    cfg = g_force_cfg >= 0 ? g_force_cfg : gemm_env_cfg();
+    if (cfg < 0) cfg = pick_cfg(a);
+  }
+  switch (cfg) {
+    case 1: launch_cfg<TC, EPI, 128, 128, 2, 2, 2>(a, st); break;
+    case 2: launch_cfg<TC, EPI, 128, 256, 2, 4, 3>(a, st); break;
+    case 3: launch_cfg<TC, EPI, 192, 256, 2, 4, 2>(a, st); break;
+    case 4: launch_cfg<TC, EPI, 256, 128, 4, 2, 3>(a, st); break;
+    case 5: launch_cfg<TC, EPI, 192, 128, 2, 2, 2>(a, st); break;
+    case 6: launch_cfg<TC, EPI, 128, 128, 4, 2, 3>(a, st); break;
+    case 7: launch_cfg<TC, EPI, 256, 256, 2, 4, 2>(a, st); break;
+    default: launch_cfg<TC, EPI, 64, 128, 2, 2, 3>(a, st); break;
   }
   return hipGetLastError();
 }
@@ -364,6 +412,8 @@ static hipError_t launch_epi(int epi, const GemmArgs& a, hipStream_t st) {
   }
   return hipErrorInvalidValue;
 }
+
+void gemm_force_config(int cfg) { g_force_cfg = cfg; }
 
 hipError_t gemm(int compute, int epi, const GemmArgs& a, hipStream_t st) {
   const int bke = compute ? 64 : 32;

@@ -36,6 +36,8 @@ struct GemmArgs {
 
 // compute: 0 fp32 operands, 1 bf16 operands. A and W both in the operand dtype.
 hipError_t gemm(int compute, int epi, const GemmArgs& a, hipStream_t st);
+// pin the bf16 GEMM tile configuration (-1 = automatic choice); tuning and test hook
+void gemm_force_config(int cfg);
 
 // attention: Q,K,V [S,H,L,64] operand dtype; O [S,L,H*64] operand dtype.
 struct AttnArgs {

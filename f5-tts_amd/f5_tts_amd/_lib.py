@@ -32,11 +32,12 @@ EXPORTS = (
     "f5h_probe_read",
     "f5h_op_linear",
     "f5h_op_attention",
+    "f5h_gemm_force_config",
     "f5h_last_error",
     "f5h_version",
 )
 
-KCLASS = {"ffn1": 0, "attention": 1, "qkv": 2, "ffn2": 3, "conv": 4}
+KCLASS = {"ffn1": 0, "attention": 1, "qkv": 2, "ffn2": 3, "conv": 4, "out": 5, "norm": 6}
 
 
 class Arch(ctypes.Structure):
@@ -103,6 +104,8 @@ def lib():
     L.f5h_op_linear.restype = ctypes.c_int
     L.f5h_op_attention.argtypes = [vp, i32, i32, i32, i32, vp, vp, vp, vp, vp, vp, sz]
     L.f5h_op_attention.restype = ctypes.c_int
+    L.f5h_gemm_force_config.argtypes = [i32]
+    L.f5h_gemm_force_config.restype = ctypes.c_int
     L.f5h_last_error.argtypes = []
     L.f5h_last_error.restype = ctypes.c_char_p
     L.f5h_version.argtypes = []

@@ -180,3 +180,8 @@ def op_attention(Q, K, V, kv_len=None, compute="bf16"):
                                            K.contiguous().data_ptr(), V.contiguous().data_ptr(), _lib.ptr(kv),
                                            O.data_ptr(), ws.data_ptr(), ws.numel()), "f5h_op_attention")
     return O
+
+
+def gemm_force_config(cfg: int = -1):
+    """Pin the bf16 GEMM tile configuration (0..7) for this process; -1 = automatic."""
+    _lib.check(_lib.lib().f5h_gemm_force_config(int(cfg)), "gemm_force_config")

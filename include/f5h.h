@@ -122,7 +122,8 @@ int f5h_forward(f5h_engine* eng, void* stream, const f5h_forward_args* args, voi
 
 /* Kernel probe: when enabled the engine brackets every launch of kernel class `kclass`
  * with HIP events on the launch stream; f5h_probe_read returns (launches, total ms).
- * Classes: 0 = FFN1 GEMM, 1 = attention, 2 = QKV GEMM, 3 = FFN2 GEMM, 4 = conv. */
+ * Classes: 0 = FFN1 GEMM, 1 = attention, 2 = QKV GEMM, 3 = FFN2 GEMM, 4 = conv,
+ * 5 = attention output-projection GEMM, 6 = pre-FFN norm (LayerNorm+modulate / RMSNorm). */
 int f5h_probe_enable(f5h_engine* eng, int32_t kclass, int32_t enable);
 int f5h_probe_read(f5h_engine* eng, int64_t* launches, double* total_ms);
 
@@ -135,6 +136,10 @@ int f5h_op_linear(void* stream, int32_t compute, int32_t M, int32_t N, int32_t K
 int f5h_op_attention(void* stream, int32_t compute, int32_t S, int32_t H, int32_t N, const float* Q,
                      const float* K, const float* V, const int32_t* kv_len, float* O, void* workspace,
                      size_t workspace_bytes);
+
+/* Tuning/test hook: pin the bf16 GEMM tile configuration for all later launches in this
+ * process (0..7), or -1 to restore the automatic per-shape choice. */
+int f5h_gemm_force_config(int32_t cfg);
 
 const char* f5h_last_error(void);
 const char* f5h_version(void);

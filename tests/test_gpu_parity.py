@@ -13,7 +13,7 @@ import torch
 
 import golden_cases as gc
 from f5_tts_amd import synthetic
-from f5_tts_amd.engine import op_attention, op_linear
+from f5_tts_amd.engine import gemm_force_config, op_attention, op_linear
 from f5_tts_amd.model import CFM, DiT, UNetT
 
 pytestmark = pytest.mark.gpu
@@ -63,6 +63,59 @@ def test_op_linear(compute, tol, M, N, K):
     ref = A.double() @ W.double().t() + b.double()
     err = (C.double() - ref).abs().max().item() / ref.abs().max().item()
     assert err < tol, err
+
+
+GEMM_CONFIGS = range(8)
+
+
+@pytest.mark.parametrize("M,N,K", [(3752, 3072, 1024), (77, 100, 1024), (3752, 1024, 2048), (700, 2048, 128)])
+def test_op_linear_every_tile_config(M, N, K):
+    """Every bf16 tile configuration meets the fp64 reference and all of them agree bit for
+    bit (same per-element K order: one lane, k-steps in sequence)."""
+    _need_gpu()
+    g = torch.Generator(device="cpu").manual_seed(M * 7 + N + K)
+    A = torch.randn(M, K, generator=g).to(DEV)
+    W = (torch.randn(N, K, generator=g) / K ** 0.5).to(DEV)
+    b = torch.randn(N, generator=g).to(DEV)
+    ref = A.double() @ W.double().t() + b.double()
+    outs = []
+    try:
+        for cfg in GEMM_CONFIGS:
+            gemm_force_config(cfg)
+            C = op_linear(A, W, b, compute="bf16")
+            err = (C.double() - ref).abs().max().item() / ref.abs().max().item()
+            assert err < 2e-2, (cfg, err)
+            outs.append(C)
+    finally:
+        gemm_force_config(-1)
+    for cfg, C in zip(GEMM_CONFIGS, outs):
+        assert torch.equal(C, outs[0]), cfg
+
+
+def test_sample_bitwise_identical_across_tile_configs():
+    """All GEMM epilogues (QKV+RoPE, gated residual, GELU, input projection) under every tile
+    configuration: a Base-architecture sample is bitwise identical."""
+    _need_gpu()
+    from f5_tts_amd import configs
+
+    arch = configs.get_arch("F5TTS_v1_Base")
+    m = _model(arch, "bf16")
+    inp = synthetic.make_case(B=2, ref_frames=[200, 150], total_frames=[700, 610], n_text=[90, 70])
+    dur = torch.tensor([700, 610])
+    y0 = synthetic.reference_noise(dur, 5)
+    kw = dict(steps=2, cfg_strength=2.0, sway_sampling_coef=-1.0, keep_trajectory=False)
+    outs = []
+    try:
+        for cfg in GEMM_CONFIGS:
+            gemm_force_config(cfg)
+            out, _ = m.sample(cond=inp["cond"].to(DEV), text=inp["text"].to(DEV), duration=dur.to(DEV),
+                              lens=inp["lens"].to(DEV), y0=y0.to(DEV), **kw)
+            outs.append(out)
+    finally:
+        gemm_force_config(-1)
+    assert torch.isfinite(outs[0]).all()
+    for cfg, o in zip(GEMM_CONFIGS, outs):
+        assert torch.equal(o, outs[0]), cfg
 
 
 @pytest.mark.parametrize("compute,tol", [("fp32", 1e-5), ("bf16", 2e-2)])

@@ -1,0 +1,67 @@
+"""Time every bf16 GEMM tile configuration on the path's GEMM shapes.
+
+Run under rocprofv3 (kernel trace), then report from the trace:
+  rocprofv3 --kernel-trace --output-format csv -d gpurun_out/gt -o run -- python tools/gemm_tune.py
+  python tools/gemm_tune.py --report gpurun_out/gt/run_kernel_trace.csv
+Dispatches are keyed by (tile template, grid), which is unique per (shape, config) here.
+"""
+import argparse
+import csv
+import os
+import sys
+
+sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..", "f5-tts_amd"))
+
+SHAPES = {  # name: (M, N, K); C2 = 2 x 1876 rows, C3 = 64 x 1876 rows
+    "c2_qkv": (3752, 3072, 1024), "c2_ffn1": (3752, 2048, 1024), "c2_out": (3752, 1024, 1024),
+    "c2_ffn2": (3752, 1024, 2048), "c3_qkv": (120064, 3072, 1024), "c3_ffn2": (120064, 1024, 2048),
+}
+CFGS = {0: (64, 128, 256), 1: (128, 128, 256), 2: (128, 256, 512), 3: (192, 256, 512), 4: (256, 128, 512),
+        5: (192, 128, 256), 6: (128, 128, 512), 7: (256, 256, 512)}
+REPS = 20
+
+
+def grid_threads(M, N, cfg):
+    bm, bn, th = CFGS[cfg]
+    return ((M + bm - 1) // bm) * ((N + bn - 1) // bn) * th
+
+
+def run():
+    import torch
+    from f5_tts_amd.engine import gemm_force_config, op_linear
+
+    dev = "cuda:0"
+    for name, (M, N, K) in SHAPES.items():
+        A = torch.randn(M, K, device=dev)
+        W = torch.randn(N, K, device=dev) / K ** 0.5
+        for cfg in CFGS:
+            gemm_force_config(cfg)
+            for _ in range(REPS):
+                op_linear(A, W, None, compute="bf16")
+        torch.cuda.synchronize()
+        print(f"done {name}", flush=True)
+    gemm_force_config(-1)
+
+
+def report(path):
+    """The gemm dispatches in issue order are SHAPES x CFGS x REPS (run() order)."""
+    rows = sorted(csv.DictReader(open(path)), key=lambda r: int(r["Start_Timestamp"]))
+    ts = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3 for r in rows
+          if "gemm_kernel" in r["Kernel_Name"]]
+    assert len(ts) == len(SHAPES) * len(CFGS) * REPS, len(ts)
+    k = 0
+    for name, (M, N, K) in SHAPES.items():
+        line = []
+        for cfg in CFGS:
+            t = sorted(ts[k:k + REPS])[: REPS * 3 // 4]  # drop the slowest quarter (cold caches)
+            k += REPS
+            avg = sum(t) / len(t)
+            line.append(f"cfg{cfg} {avg:8.2f}us {2 * M * N * K / avg / 1e6:5.0f}TF")
+        print(f"{name:8s} " + " | ".join(line))
+
+
+if __name__ == "__main__":
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--report")
+    a = ap.parse_args()
+    report(a.report) if a.report else run()
