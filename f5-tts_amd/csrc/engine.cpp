@@ -858,13 +858,25 @@ int f5h_op_linear(void* stream, int32_t compute, int32_t M, int32_t N, int32_t K
 }
 
 int f5h_gemm_force_config(int32_t cfg) {
-  if (cfg < -1 || cfg > 7) return fail(F5H_EINVAL, "gemm config must be -1..7");
+  if (cfg < -1 || (cfg > 7 && cfg < 10) || cfg > 17) return fail(F5H_EINVAL, "gemm config must be -1..7 or 10..17");
   gemm_force_config(cfg);
   return 0;
 }
 
+int f5h_debug_attn_stamps(uint64_t* out, int32_t n) {
+  HIPCK(attn_read_stamps(out, n));
+  return 0;
+}
+
+int f5h_attn_force_variant(int32_t v) {
+  if (v != -1 && (v < 1 || v > 8)) return fail(F5H_EINVAL, "attention variant must be -1 or 1..8");
+  attn_force_variant(v);
+  return 0;
+}
+
 int f5h_op_attention(void* stream, int32_t compute, int32_t S, int32_t H, int32_t N, const float* Q, const float* K,
-                     const float* V, const int32_t* kv_len, float* O, void* workspace, size_t workspace_bytes) {
+                     const float* V, const int32_t* kv_len, int32_t q_prescaled, float* O, void* workspace,
+                     size_t workspace_bytes) {
   if (S <= 0 || H <= 0 || N <= 0) return fail(F5H_EINVAL, "bad attention shape");
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   const int64_t n = (int64_t)S * H * N * 64;
@@ -874,6 +886,7 @@ int f5h_op_attention(void* stream, int32_t compute, int32_t S, int32_t H, int32_
   at.L = N;
   at.kv_len = kv_len;
   at.scale = 0.125f;
+  at.prescaled = q_prescaled ? 1 : 0;
   if (compute) {
     const size_t need = (size_t)n * 2 * 4 + 4 * 256;
     if (workspace_bytes < need) return fail(F5H_ENOMEM, "workspace too small for op_attention");

@@ -48,6 +48,9 @@ struct AttnArgs {
   int prescaled;          // q already carries scale*log2(e): scores are in log2 units
 };
 hipError_t attention(int compute, const AttnArgs& a, hipStream_t st);
+// pin the bf16 attention variant (-1 = default); tuning and test hook
+void attn_force_variant(int v);
+hipError_t attn_read_stamps(uint64_t* host, int n);  // variant 6 diagnostic stamps
 
 // grouped conv1d k=31, 16 groups, pad 15 (ConvPositionEmbedding, modules.py:175-201)
 struct ConvArgs {

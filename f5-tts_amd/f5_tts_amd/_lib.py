@@ -33,6 +33,8 @@ EXPORTS = (
     "f5h_op_linear",
     "f5h_op_attention",
     "f5h_gemm_force_config",
+    "f5h_attn_force_variant",
+    "f5h_debug_attn_stamps",
     "f5h_last_error",
     "f5h_version",
 )
@@ -102,10 +104,14 @@ def lib():
     L.f5h_probe_read.restype = ctypes.c_int
     L.f5h_op_linear.argtypes = [vp, i32, i32, i32, i32, vp, vp, vp, vp, vp, sz]
     L.f5h_op_linear.restype = ctypes.c_int
-    L.f5h_op_attention.argtypes = [vp, i32, i32, i32, i32, vp, vp, vp, vp, vp, vp, sz]
+    L.f5h_op_attention.argtypes = [vp, i32, i32, i32, i32, vp, vp, vp, vp, i32, vp, vp, sz]
     L.f5h_op_attention.restype = ctypes.c_int
     L.f5h_gemm_force_config.argtypes = [i32]
     L.f5h_gemm_force_config.restype = ctypes.c_int
+    L.f5h_attn_force_variant.argtypes = [i32]
+    L.f5h_attn_force_variant.restype = ctypes.c_int
+    L.f5h_debug_attn_stamps.argtypes = [vp, i32]
+    L.f5h_debug_attn_stamps.restype = ctypes.c_int
     L.f5h_last_error.argtypes = []
     L.f5h_last_error.restype = ctypes.c_char_p
     L.f5h_version.argtypes = []

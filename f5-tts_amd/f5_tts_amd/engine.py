@@ -169,7 +169,8 @@ def op_linear(A, W, bias=None, compute="bf16"):
     return C
 
 
-def op_attention(Q, K, V, kv_len=None, compute="bf16"):
+def op_attention(Q, K, V, kv_len=None, compute="bf16", q_prescaled=False):
+    """O[S,N,H*64] = softmax(Q K^T/8) V; q_prescaled: Q already carries (1/8)*log2(e)."""
     S, H, N, D = Q.shape
     assert D == 64
     O = torch.empty(S, N, H * 64, dtype=torch.float32, device=Q.device)
@@ -178,10 +179,16 @@ def op_attention(Q, K, V, kv_len=None, compute="bf16"):
     kv = None if kv_len is None else kv_len.to(Q.device, torch.int32).contiguous()
     _lib.check(_lib.lib().f5h_op_attention(_lib.stream_handle(Q.device), c, S, H, N, Q.contiguous().data_ptr(),
                                            K.contiguous().data_ptr(), V.contiguous().data_ptr(), _lib.ptr(kv),
-                                           O.data_ptr(), ws.data_ptr(), ws.numel()), "f5h_op_attention")
+                                           int(bool(q_prescaled)), O.data_ptr(), ws.data_ptr(), ws.numel()),
+               "f5h_op_attention")
     return O
 
 
 def gemm_force_config(cfg: int = -1):
-    """Pin the bf16 GEMM tile configuration (0..7) for this process; -1 = automatic."""
+    """Pin the bf16 GEMM tile configuration (0..7, 10..17) for this process; -1 = automatic."""
     _lib.check(_lib.lib().f5h_gemm_force_config(int(cfg)), "gemm_force_config")
+
+
+def attn_force_variant(v: int = -1):
+    """Pin the bf16 attention kernel variant (1, 2, 3) for this process; -1 = default."""
+    _lib.check(_lib.lib().f5h_attn_force_variant(int(v)), "attn_force_variant")

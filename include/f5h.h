@@ -132,14 +132,21 @@ int f5h_probe_read(f5h_engine* eng, int64_t* launches, double* total_ms);
 int f5h_op_linear(void* stream, int32_t compute, int32_t M, int32_t N, int32_t K, const float* A,
                   const float* W, const float* bias, float* C, void* workspace, size_t workspace_bytes);
 /* O[S,N,H*64] = softmax(Q K^T / 8 [+key mask]) V with Q,K,V [S,H,N,64] fp32;
- * kv_len: [S] valid keys per sequence or NULL. */
+ * kv_len: [S] valid keys per sequence or NULL. q_prescaled != 0: Q already carries
+ * scale * log2(e) (the engine's layout: scores in log2 units). */
 int f5h_op_attention(void* stream, int32_t compute, int32_t S, int32_t H, int32_t N, const float* Q,
-                     const float* K, const float* V, const int32_t* kv_len, float* O, void* workspace,
-                     size_t workspace_bytes);
+                     const float* K, const float* V, const int32_t* kv_len, int32_t q_prescaled, float* O,
+                     void* workspace, size_t workspace_bytes);
 
 /* Tuning/test hook: pin the bf16 GEMM tile configuration for all later launches in this
- * process (0..7), or -1 to restore the automatic per-shape choice. */
+ * process (0..7, 10..17), or -1 to restore the automatic per-shape choice. */
 int f5h_gemm_force_config(int32_t cfg);
+/* Tuning/test hook: pin the bf16 attention kernel variant (1, 2, 3), or -1
+ * to restore the default. */
+int f5h_attn_force_variant(int32_t variant);
+/* Diagnostic: per-segment cycle sums of the last variant-6 attention launch (first 4 (s,head)
+ * pairs x 8 waves x 8 words). */
+int f5h_debug_attn_stamps(uint64_t* out, int32_t n);
 
 const char* f5h_last_error(void);
 const char* f5h_version(void);

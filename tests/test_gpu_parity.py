@@ -13,7 +13,7 @@ import torch
 
 import golden_cases as gc
 from f5_tts_amd import synthetic
-from f5_tts_amd.engine import gemm_force_config, op_attention, op_linear
+from f5_tts_amd.engine import attn_force_variant, gemm_force_config, op_attention, op_linear
 from f5_tts_amd.model import CFM, DiT, UNetT
 
 pytestmark = pytest.mark.gpu
@@ -65,7 +65,7 @@ def test_op_linear(compute, tol, M, N, K):
     assert err < tol, err
 
 
-GEMM_CONFIGS = range(8)
+GEMM_CONFIGS = list(range(8)) + list(range(10, 18))  # 10+: ping-pong 8-wave kernels
 
 
 @pytest.mark.parametrize("M,N,K", [(3752, 3072, 1024), (77, 100, 1024), (3752, 1024, 2048), (700, 2048, 128)])
@@ -134,6 +134,42 @@ def test_op_attention(compute, tol, S, H, N, masked):
     ref = ref.transpose(1, 2).reshape(S, N, H * 64)
     err = (O.double() - ref).abs().max().item() / ref.abs().max().item()
     assert err < tol, err
+
+
+ATTN_VARIANTS = [1, 2, 3, 4, 5, 7]
+
+
+@pytest.mark.parametrize("variant", ATTN_VARIANTS)
+@pytest.mark.parametrize("spike", [0.0, 12.0, 160.0])
+def test_op_attention_variants_and_rare_branches(variant, spike):
+    """Every bf16 attention variant against an fp64 softmax of the SAME bf16 operands (the
+    engine's layout: q pre-multiplied by (1/8)*log2(e), scores in log2 units), with inputs that
+    force the rare branches (cdna_hip_programming.md rule 26): one key row at a late tile is
+    aligned with a few query rows so their scores jump far above the first tile's. spike 12:
+    past the lazy-rescale threshold (2^8) of v2/v3; spike 160: ~160 log2 units, beyond the
+    fixed-offset range of v4/v5/v6, whose waves must fall back to the exact per-row loop."""
+    _need_gpu()
+    S, H, N = 2, 2, 700
+    g = torch.Generator(device="cpu").manual_seed(11)
+    Q, K, V = (torch.randn(S, H, N, 64, generator=g) for _ in range(3))
+    Q = Q * (0.125 * 1.4426950408889634)
+    if spike:
+        for key, qs in ((650, (5, 6, 7)), (400, (300,))):
+            for qi in qs:
+                K[:, :, key] += spike * Q[:, :, qi] / Q[:, :, qi].pow(2).sum(-1, keepdim=True)
+    Q, K, V = (x.bfloat16().float() for x in (Q, K, V))
+    sc = Q.double() @ K.double().transpose(-1, -2)
+    p = torch.exp2(sc - sc.amax(-1, keepdim=True))
+    ref = (p / p.sum(-1, keepdim=True)) @ V.double()
+    ref = ref.transpose(1, 2).reshape(S, N, H * 64)
+    try:
+        attn_force_variant(variant)
+        O = op_attention(Q.to(DEV), K.to(DEV), V.to(DEV), None, compute="bf16", q_prescaled=True).cpu()
+    finally:
+        attn_force_variant(-1)
+    assert torch.isfinite(O).all()
+    err = ((O.double() - ref).abs().max() / ref.abs().max()).item()
+    assert err < 1e-2, err
 
 
 # ---------------------------------------------------------------- backbone forward vs reference

@@ -17,7 +17,9 @@ SHAPES = {  # name: (M, N, K); C2 = 2 x 1876 rows, C3 = 64 x 1876 rows
     "c2_ffn2": (3752, 1024, 2048), "c3_qkv": (120064, 3072, 1024), "c3_ffn2": (120064, 1024, 2048),
 }
 CFGS = {0: (64, 128, 256), 1: (128, 128, 256), 2: (128, 256, 512), 3: (192, 256, 512), 4: (256, 128, 512),
-        5: (192, 128, 256), 6: (128, 128, 512), 7: (256, 256, 512)}
+        5: (192, 128, 256), 6: (128, 128, 512), 7: (256, 256, 512),
+        10: (256, 256, 512), 11: (256, 192, 512), 12: (256, 128, 512), 13: (128, 128, 512), 14: (128, 128, 512),
+        15: (256, 64, 512), 16: (128, 256, 512), 17: (256, 256, 512)}
 REPS = 20
 
 
@@ -47,7 +49,7 @@ def report(path):
     """The gemm dispatches in issue order are SHAPES x CFGS x REPS (run() order)."""
     rows = sorted(csv.DictReader(open(path)), key=lambda r: int(r["Start_Timestamp"]))
     ts = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3 for r in rows
-          if "gemm_kernel" in r["Kernel_Name"]]
+          if "gemm_" in r["Kernel_Name"]]
     assert len(ts) == len(SHAPES) * len(CFGS) * REPS, len(ts)
     k = 0
     for name, (M, N, K) in SHAPES.items():
@@ -56,8 +58,10 @@ def report(path):
             t = sorted(ts[k:k + REPS])[: REPS * 3 // 4]  # drop the slowest quarter (cold caches)
             k += REPS
             avg = sum(t) / len(t)
-            line.append(f"cfg{cfg} {avg:8.2f}us {2 * M * N * K / avg / 1e6:5.0f}TF")
-        print(f"{name:8s} " + " | ".join(line))
+            line.append(f"cfg{cfg:<2d} {avg:8.2f}us {2 * M * N * K / avg / 1e6:5.0f}TF")
+        print(f"{name:8s}")
+        for i in range(0, len(line), 8):
+            print("   " + " | ".join(line[i:i + 8]))
 
 
 if __name__ == "__main__":
