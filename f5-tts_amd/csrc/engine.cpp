@@ -869,7 +869,7 @@ int f5h_debug_attn_stamps(uint64_t* out, int32_t n) {
 }
 
 int f5h_attn_force_variant(int32_t v) {
-  if (v != -1 && (v < 1 || v > 8)) return fail(F5H_EINVAL, "attention variant must be -1 or 1..8");
+  if (v != -1 && (v < 1 || v > 9)) return fail(F5H_EINVAL, "attention variant must be -1 or 1..9");
   attn_force_variant(v);
   return 0;
 }
