@@ -1,4 +1,4 @@
-"""Benchmark: F5-TTS Base (v1) CFM.sample on MI355X through the HIP engine.
+"""Benchmark: F5-TTS CFM.sample on MI355X through the HIP engine.
 
 Workload (BASELINE.json configs[1] = SURVEY C2): F5TTS_v1_Base, bf16 MFMA engine, NFE 16
 (EPSS grid) + sway -1, CFG 2.0, B=1 per GPU, 10 s prompt (938 ref frames) + 938 generated
@@ -7,10 +7,12 @@ embedding, 16 packed cond/uncond DiT forwards, CFG + Euler, final cond overwrite
 RCCL all-gather of the finished mels. Synthetic data and hash-PRNG weights of the real
 architecture (checkpoints are network-only).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c3|c5]
     torchrun --nproc-per-node N bench.py --gpus N ...   (one rank per GPU, weak scaling)
 
-Prints ONE JSON line on rank 0 (contract in the task statement).
+Prints ONE JSON line on rank 0 (contract in the task statement). The default (and the driver's)
+workload is C2; --config c3 (B=32 mixed lengths, NFE 32, batch-mask path) and c5 (E2 UNetT,
+B=8) measure the other BASELINE.json configs the same way (no CPU baseline for those).
 """
 
 from __future__ import annotations
@@ -35,6 +37,32 @@ PEAK_BF16_TFLOPS = 2500.0  # MI355X dense bf16 MFMA (MI355X_MICROARCH.md chip ta
 
 def attn_flops(S, H, L):
     return 4.0 * S * H * L * L * 64  # QK^T + PV per launch
+
+
+def seq_flops(arch, N):
+    """Algorithmic FLOPs of one sequence-forward at padded length N (linear part per
+    token + attention part; DiT Base: 378.888e6 N + 90112 N^2; E2 UNetT attends over N+1)."""
+    d, depth, ff = arch["dim"], arch["depth"], int(arch["dim"] * arch["ff_mult"])
+    per_tok = depth * (8.0 * d * d + 4.0 * d * ff) + 2.0 * 2 * 31 * 64 * d + 2.0 * d * arch["mel_dim"]
+    if arch["backbone"] == "DiT":
+        L = N
+        per_tok += 2.0 * (2 * arch["mel_dim"] + arch["text_dim"]) * d
+    else:
+        L = N + 1
+        per_tok += (depth // 2) * 2.0 * 2 * d * d + 2.0 * (2 * arch["mel_dim"] + arch["text_dim"]) * d
+    return per_tok * L + 4.0 * depth * d * L * L
+
+
+def pmc_traffic(kernel_class):
+    """HBM bytes per launch of the probed kernel from the committed rocprofv3 PMC summary
+    (profiles/*_pmc_<class>.json, written by tools/profile_round.sh): FETCH_SIZE doubled (it
+    reads 1/2 of wide streaming reads on gfx950, MI355X_MICROARCH.md §HBM) + WRITE_SIZE."""
+    import glob
+    files = sorted(glob.glob(os.path.join(REPO, "profiles", f"*_pmc_{kernel_class}.json")))
+    if not files:
+        return None, None
+    d = json.load(open(files[-1]))
+    return (2.0 * d["fetch_size_kb"] + d["write_size_kb"]) * 1024.0, os.path.relpath(files[-1], REPO)
 
 
 def build_model(preset, compute, device):
@@ -90,6 +118,8 @@ def main():
     ap.add_argument("--compute", default="bf16")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--probe", default="attention", help="kernel class timed with HIP events for the roofline")
+    ap.add_argument("--config", default="c2", choices=("c2", "c3", "c5"),
+                    help="workload (SURVEY §8d); c2 is the headline line")
     ap.add_argument("--probe-all", action="store_true",
                     help="after the measurement, time every kernel class in its own loop (table on stderr)")
     args = ap.parse_args()
@@ -105,20 +135,24 @@ def main():
     device = torch.device("cuda", local)
     torch.cuda.set_device(device)
 
-    case = synthetic.c2_case()
-    case["preset"] = args.preset
-    model, arch = build_model(args.preset, args.compute, device)
-    inp = synthetic.make_case(B=1, ref_frames=case["ref"], total_frames=case["total"], n_text=case["nt"],
-                              seed=1234 + rank)
+    case = {"c2": synthetic.c2_case, "c3": synthetic.c3_case, "c5": synthetic.c5_case}[args.config]()
+    if args.config == "c2":
+        case["preset"] = args.preset
+    model, arch = build_model(case["preset"], args.compute, device)
+    B = case["B"]
+    refs = case["ref"] if isinstance(case["ref"], list) else [case["ref"]] * B
+    tots = case["total"] if isinstance(case["total"], list) else [case["total"]] * B
+    inp = synthetic.make_case(B=B, ref_frames=refs, total_frames=tots, n_text=case["nt"], seed=1234 + rank)
     cond, text = inp["cond"].to(device), inp["text"].to(device)
     duration, lens = inp["duration"].to(device), inp["lens"].to(device)
-    gen_frames = case["total"] - case["ref"]
-    gathered = torch.empty(world, gen_frames, 100, device=device)
+    gen_frames = sum(t - r for t, r in zip(tots, refs))
+    Nmax = max(tots)
+    gathered = torch.empty(world, gen_frames * 100, device=device)
 
     def step():
         out, _ = model.sample(cond=cond, text=text, duration=duration, lens=lens, steps=case["nfe"],
                               cfg_strength=case["cfg"], sway_sampling_coef=case["sway"], seed=rank)
-        mel = out[0, case["ref"]:].contiguous()
+        mel = torch.cat([out[b, refs[b]:tots[b]].reshape(-1) for b in range(B)])
         if world > 1:
             dist.all_gather_into_tensor(gathered, mel)  # finished mels only
         return mel
@@ -151,14 +185,18 @@ def main():
     ms_per_step = elapsed / args.steps * 1e3
     rtf = elapsed / (frames * HOP / SR) * world  # wall / generated audio seconds, per GPU stream
 
-    S, H, L = 2, arch["heads"], case["total"]
+    S = 2 * B if case["cfg"] >= 1e-5 else B
+    H = arch["heads"]
+    L = Nmax if arch["backbone"] == "DiT" else Nmax + 1
     roof = None
     if n_launch:
         avg_ms = probe_ms / n_launch
         fl = class_flops(args.probe, arch, S, L)
         ach = fl / (avg_ms * 1e-3) / 1e12 if fl else 0.0
+        traffic, tsrc = pmc_traffic(args.probe) if args.config == "c2" else (None, None)
         roof = {"bound": "mfma", "kernel": args.probe, "achieved": round(ach, 2), "peak": PEAK_BF16_TFLOPS,
-                "unit": "TFLOP/s", "frac": round(ach / PEAK_BF16_TFLOPS, 4), "traffic": None,
+                "unit": "TFLOP/s", "frac": round(ach / PEAK_BF16_TFLOPS, 4), "traffic": traffic,
+                "traffic_unit": "bytes/launch", "traffic_source": tsrc,
                 "avg_launch_ms": round(avg_ms, 5), "launches": n_launch, "flops_per_launch": fl}
 
     if args.probe_all and rank == 0:
@@ -177,14 +215,22 @@ def main():
                       + (f"  {fl / (avg * 1e-3) / 1e12:7.1f} TF/s" if fl else ""), file=sys.stderr, flush=True)
 
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and args.config == "c2":
         cpu = cpu_baseline(case, arch, threads=min(16, os.cpu_count() or 1))
 
-    # whole-path algorithmic FLOPs: NFE * S * F(N), F(N) = 378.888e6 N + 90112 N^2 (Base)
-    flops_call = case["nfe"] * S * (378.888e6 * L + 90112.0 * L * L)
+    # whole-path algorithmic FLOPs: NFE * S * F(N) at the padded length
+    flops_call = case["nfe"] * S * seq_flops(arch, Nmax)
     if rank == 0:
+        workloads = {
+            "c2": "C2: F5TTS_v1_Base CFM.sample, NFE 16 EPSS + sway -1, CFG 2.0, 1 utterance per GPU, "
+                  "938 prompt + 938 generated frames (1876), 300 tokens",
+            "c3": "C3: F5TTS_v1_Base CFM.sample, NFE 32 linspace + sway -1, CFG 2.0, 32 utterances per GPU, "
+                  "564..1876 frames (half prompt), padded to 1876, batch-mask path",
+            "c5": "C5: E2TTS_Base (UNetT) CFM.sample, NFE 16 EPSS + sway -1, CFG 2.0, 8 utterances per GPU, "
+                  "938 prompt + 938 generated frames, 300 tokens",
+        }
         line = {
-            "metric": "mel-frames/s (RTF alongside), F5-TTS Base NFE=16 CFM.sample",
+            "metric": f"mel-frames/s (RTF alongside), {case['preset']} NFE={case['nfe']} CFM.sample",
             "value": round(value, 2),
             "unit": "mel-frames/s",
             "n_gpus": world,
@@ -195,11 +241,9 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": args.compute,
-            "data": "synthetic (hash-PRNG weights of F5TTS_v1_Base, N(-4,2) cond mel, uniform text ids)",
-            "config": {"workload": "C2: F5TTS_v1_Base CFM.sample, NFE 16 EPSS + sway -1, CFG 2.0, 1 utterance "
-                                   "per GPU, 938 prompt + 938 generated frames (1876), 300 tokens",
-                       "batch_per_gpu": 1, "frames": L, "gen_frames": gen_frames, "nfe": case["nfe"],
-                       "parallelism": f"dp{world}"},
+            "data": f"synthetic (hash-PRNG weights of {case['preset']}, N(-4,2) cond mel, uniform text ids)",
+            "config": {"workload": workloads[args.config], "batch_per_gpu": B, "frames": Nmax,
+                       "gen_frames": gen_frames, "nfe": case["nfe"], "parallelism": f"dp{world}"},
             "rtf": round(rtf, 5),
             "path_tflops": round(flops_call * args.steps * world / elapsed / 1e12, 2),
             "roofline": roof,

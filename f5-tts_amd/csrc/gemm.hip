@@ -71,7 +71,7 @@ F5H_DEV V8 load8(const float* p) {
 
 // Apply the epilogue to 8 consecutive columns [col, col+8) of output row `row`.
 template <typename TC, int EPI>
-F5H_DEV void epi8(const GemmArgs& g, int row, int col, V8 x) {
+F5H_DEV void epi8(const GemmArgs& g, int row, int col, V8 x, const V8* pre = nullptr) {
   const bool full = col + 8 <= g.N;
   if (g.bias) {
     if (full) {
@@ -133,7 +133,7 @@ F5H_DEV void epi8(const GemmArgs& g, int row, int col, V8 x) {
       for (int e = 0; e < 8; ++e) x.v[e] = gelu_erf(x.v[e]);
     } else if constexpr (EPI == EPI_RESID) {
       const float keep = (g.rowkeep && !g.rowkeep[row]) ? 0.f : 1.f;
-      V8 c = vec ? load8(C + off) : V8{};
+      V8 c = vec ? (pre ? *pre : load8(C + off)) : V8{};
       if (!vec)
         for (int e = 0; e < 8; ++e) c.v[e] = col + e < g.N ? C[off + e] : 0.f;
       V8 gt = g.gate ? (full ? load8(g.gate + col) : V8{}) : V8{{1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f}};
@@ -258,6 +258,29 @@ __global__ __launch_bounds__(64 * WGM * WGN, 1) void gemm_kernel(GemmArgs g) {
 #pragma unroll
     for (int j = 0; j < NT; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
+  // EPI_RESID: the residual rows this lane's epilogue reads are fetched before the K loop (the
+  // oldest VMEM ops, retired by the first stage wait), so the epilogue's read-modify-write does
+  // not expose a dependent HBM/MALL round trip. Register budget: small tiles only.
+  constexpr int CH_ = WN / 8, TPS = 16 * CH_ / 64;
+  constexpr bool PREF = EPI == EPI_RESID && std::is_same<TC, bf16>::value && (16 * CH_) % 64 == 0 &&
+                        MT * TPS * 8 <= 32;
+  V8 pre[PREF ? MT : 1][PREF ? TPS : 1];
+  if constexpr (PREF) {
+    const float* Cp = reinterpret_cast<const float*>(g.C);
+    const int fr_ = lane & 15, q_ = lane >> 4;
+    (void)fr_;
+    (void)q_;
+#pragma unroll
+    for (int i = 0; i < MT; ++i)
+#pragma unroll
+      for (int t = 0; t < TPS; ++t) {
+        const int idx = t * 64 + lane, rr = idx / CH_, cc = idx % CH_;
+        const int row = m0 + wm * WM + i * 16 + rr, col = n0 + wn * WN + cc * 8;
+        const bool ok = row < g.M && col + 8 <= g.N && g.ldc % 4 == 0;
+        pre[i][t] = ok ? load8(Cp + (int64_t)row * g.ldc + col) : V8{};
+      }
+  }
+
   const int nk = g.K / BKE;
   for (int p = 0; p < NS - 1 && p < nk; ++p) stage(p, p * BKE);
   for (int kt = 0; kt < nk; ++kt) {
@@ -328,7 +351,8 @@ __global__ __launch_bounds__(64 * WGM * WGN, 1) void gemm_kernel(GemmArgs g) {
       const int row = m0 + wm * WM + i * 16 + rr, col = n0 + wn * WN + cc * 8;
       const float* src = Cs + rr * C::EPAD + cc * 8;
       float4 a = *reinterpret_cast<const float4*>(src), b = *reinterpret_cast<const float4*>(src + 4);
-      if (row < g.M && col < g.N) epi8<TC, EPI>(g, row, col, V8{{a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w}});
+      if (row < g.M && col < g.N)
+        epi8<TC, EPI>(g, row, col, V8{{a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w}}, PREF ? &pre[PREF ? i : 0][PREF ? t : 0] : nullptr);
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
