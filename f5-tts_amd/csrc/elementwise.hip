@@ -41,6 +41,71 @@ hipError_t time_sinus(const float* t_host, int n, float* out, hipStream_t st) {
   return hipGetLastError();
 }
 
+// The ODE grid t[0..n-1] into device memory (kernel-argument upload, capturable).
+__global__ void grid_upload_kernel(TVals tv, int n, float* out) {
+  int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) out[i] = tv.t[i];
+}
+// A host pointer value into a device slot (kernel-argument upload, stream-ordered).
+__global__ void ptr_upload_kernel(float* p, float** slot) {
+  if (threadIdx.x == 0) slot[0] = p;
+}
+hipError_t ptr_upload(float* p, float** slot, hipStream_t st) {
+  hipLaunchKernelGGL(ptr_upload_kernel, dim3(1), dim3(64), 0, st, p, slot);
+  return hipGetLastError();
+}
+hipError_t grid_upload(const float* t_host, int n, float* out, hipStream_t st) {
+  if (n <= 0 || n > 512) return hipErrorInvalidValue;
+  TVals tv{};
+  for (int i = 0; i < n; ++i) tv.t[i] = t_host[i];
+  hipLaunchKernelGGL(grid_upload_kernel, dim3(nblk(n, 256)), dim3(256), 0, st, tv, n, out);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------- NFE-step bookkeeping
+// One NFE step is a fixed launch sequence (hipGraph-replayable): step_begin copies the step's
+// row of a per-call table (AdaLN shift/scale/gate rows, or the UNetT time token) to a fixed
+// buffer; step_advance bumps the device-side step index after the Euler update.
+__global__ void step_begin_kernel(const int* kstep, const float* src, int64_t stride, int n, float* dst) {
+  const int k = *kstep;
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i * 4 < n) {
+    const float4* s = reinterpret_cast<const float4*>(src + (int64_t)k * stride);
+    reinterpret_cast<float4*>(dst)[i] = s[i];
+  }
+}
+hipError_t step_begin(const int* kstep, const float* src, int64_t stride, int n, float* dst, hipStream_t st) {
+  if (n % 4 || stride % 4) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(step_begin_kernel, dim3(nblk(n / 4, 256)), dim3(256), 0, st, kstep, src, stride, n, dst);
+  return hipGetLastError();
+}
+// Probe stamps (device wall clock, s_memrealtime) around a launch inside a step graph.
+__global__ void stamp_begin_kernel(unsigned long long* slot) {
+  if (threadIdx.x == 0) slot[0] = wall_clock64();
+}
+__global__ void stamp_end_kernel(const unsigned long long* slot, unsigned long long* acc) {
+  if (threadIdx.x == 0) {
+    const unsigned long long t = wall_clock64();
+    atomicAdd(&acc[0], t - slot[0]);
+    atomicAdd(&acc[1], 1ull);
+  }
+}
+hipError_t stamp_begin(unsigned long long* slot, hipStream_t st) {
+  hipLaunchKernelGGL(stamp_begin_kernel, dim3(1), dim3(64), 0, st, slot);
+  return hipGetLastError();
+}
+hipError_t stamp_end(const unsigned long long* slot, unsigned long long* acc, hipStream_t st) {
+  hipLaunchKernelGGL(stamp_end_kernel, dim3(1), dim3(64), 0, st, slot, acc);
+  return hipGetLastError();
+}
+__global__ void step_advance_kernel(int* kstep) {
+  if (threadIdx.x == 0) kstep[0] += 1;
+}
+hipError_t step_advance(int* kstep, hipStream_t st) {
+  hipLaunchKernelGGL(step_advance_kernel, dim3(1), dim3(64), 0, st, kstep);
+  return hipGetLastError();
+}
+
 template <typename TO>
 __global__ void silu_kernel(const float* x, TO* y, int64_t n) {
   int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -372,10 +437,18 @@ __global__ void cfg_euler_kernel(EulerArgs a, TO* ypad) {
     const float pu = a.p[(int64_t)(a.B + b) * a.p_seq_stride + (int64_t)(a.p_row_off + n) * a.p_ld + c];
     v = __fadd_rn(pc, __fmul_rn(__fsub_rn(pc, pu), a.cfg));
   }
-  const float y = __fadd_rn(a.y[i], __fmul_rn(a.dt, v));
+  float dt = a.dt;
+  float* traj = a.traj;
+  if (a.kstep) {  // graph-replayable form: step index, grid and trajectory base live on the device
+    const int k = *a.kstep;
+    dt = __fsub_rn(a.tgrid[k + 1], a.tgrid[k]);
+    traj = a.trajp ? *a.trajp : nullptr;
+    if (traj) traj += (int64_t)(k + 1) * total;
+  }
+  const float y = __fadd_rn(a.y[i], __fmul_rn(dt, v));
   a.y[i] = y;
   if (ypad) ypad[bn * 128 + c] = from_f32<TO>(y);
-  if (a.traj) a.traj[i] = y;
+  if (traj) traj[i] = y;
 }
 hipError_t cfg_euler(const EulerArgs& a, hipStream_t st) {
   const int64_t total = (int64_t)a.B * a.N * a.mel;
@@ -396,6 +469,20 @@ hipError_t final_where(const float* cond, const uint8_t* cond_mask, float* y, in
                        hipStream_t st) {
   const int64_t total = (int64_t)B * N * mel;
   hipLaunchKernelGGL(final_where_kernel, dim3(nblk(total, 256)), dim3(256), 0, st, cond, cond_mask, y, total, mel);
+  return hipGetLastError();
+}
+// out = where(cond_mask, cond, y) from the workspace ODE state y
+__global__ void final_where_out_kernel(const float* cond, const uint8_t* m, const float* y, float* out,
+                                       int64_t total, int mel) {
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= total) return;
+  out[i] = m[i / mel] ? cond[i] : y[i];
+}
+hipError_t final_where_out(const float* cond, const uint8_t* cond_mask, const float* y, float* out, int B, int N,
+                           int mel, hipStream_t st) {
+  const int64_t total = (int64_t)B * N * mel;
+  hipLaunchKernelGGL(final_where_out_kernel, dim3(nblk(total, 256)), dim3(256), 0, st, cond, cond_mask, y, out,
+                     total, mel);
   return hipGetLastError();
 }
 

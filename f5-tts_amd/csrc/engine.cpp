@@ -82,6 +82,13 @@ struct f5h_engine {
   float* conv_b[2] = {nullptr, nullptr};
   std::vector<Layer> layers;
   float* norm_out_g = nullptr;
+  // hipGraph cache of one NFE step (keyed by the call's buffers and shape)
+  std::mutex gm;
+  std::vector<struct GraphEntry*> graphs;
+  hipStream_t cap = nullptr;  // private capture stream (the caller's may be the null stream)
+  int graph_mode = 1;
+  uint64_t use_ctr = 0;
+  int64_t n_captures = 0, n_replays = 0;
   // probe
   std::mutex pm;
   int probe_class = -1;
@@ -89,7 +96,34 @@ struct f5h_engine {
   size_t ev_used = 0;
   int64_t probe_launches = 0;
   double probe_ms = 0.0;
+  // graph-mode probe: device wall-clock stamps (s_memrealtime) around each probed launch;
+  // pstamp[0] = sum of ticks, pstamp[1] = launches, pstamp[64 + j] = start stamp of site j
+  unsigned long long* pstamp = nullptr;
+  double wall_khz = 0.0;
 };
+static constexpr int kStampSites = 4096 - 64;
+
+// The step graph touches only workspace buffers (the ODE state, the trajectory base and the step
+// index live in the workspace), so it is keyed by the workspace and the launch shape alone.
+struct GraphKey {
+  const void* ws;
+  int B, N, nfe, use_cfg, batch_mask, probe;
+  uint32_t cfg_bits;
+  bool operator==(const GraphKey& o) const {
+    return ws == o.ws && B == o.B && N == o.N && nfe == o.nfe &&
+           use_cfg == o.use_cfg && batch_mask == o.batch_mask && probe == o.probe && cfg_bits == o.cfg_bits;
+  }
+};
+struct GraphEntry {
+  GraphKey key{};
+  hipGraphExec_t exec = nullptr;
+  uint64_t stamp = 0;
+};
+static void graph_entry_free(GraphEntry* g) {
+  if (!g) return;
+  if (g->exec) (void)hipGraphExecDestroy(g->exec);
+  delete g;
+}
 
 // ---------------------------------------------------------------- weight packing
 struct WMap {
@@ -345,6 +379,10 @@ struct Bufs {
   float2* rope;
   uint8_t* rowkeep;
   int32_t* kvlen;
+  float *ada_cur, *temb_cur, *tgrid;  // the current step's table rows; device copy of the grid
+  int* kstep;                         // device-side NFE step index
+  float* y;                           // ODE state [B][N][mel] fp32
+  float** trajp;                      // device slot: trajectory base pointer (or null)
   std::vector<void*> skips;
 };
 
@@ -387,6 +425,12 @@ static void layout(const f5h_engine* e, WS& ws, Bufs& b, int B, int N, int nfe, 
   b.rope = ws.take<float2>((size_t)L * 32);
   b.rowkeep = ws.take<uint8_t>(rows);
   b.kvlen = ws.take<int32_t>(S);
+  b.ada_cur = a.backbone == F5H_DIT ? ws.take<float>((size_t)e->ada.Npad) : nullptr;
+  b.temb_cur = ws.take<float>((size_t)d);
+  b.tgrid = ws.take<float>((size_t)nfe);
+  b.kstep = ws.take<int>(64);
+  b.y = ws.take<float>((size_t)B * N * e->a.mel_dim);
+  b.trajp = ws.take<float*>(8);
   b.skips.clear();
   if (a.backbone == F5H_UNETT)
     for (int i = 0; i < a.depth / 2; ++i) b.skips.push_back(ws.take<char>(rows * d * es));
@@ -399,7 +443,15 @@ struct ProbeScope {
   hipStream_t st;
   bool on;
   size_t idx = 0;
-  ProbeScope(f5h_engine* e_, int kc, hipStream_t s) : e(e_), st(s), on(e_->probe_class == kc) {
+  int* cap = nullptr;  // capturing a step graph: next stamp site (events cannot be timed in a graph)
+  ProbeScope(f5h_engine* e_, int kc, hipStream_t s, int* cap_ = nullptr)
+      : e(e_), st(s), on(e_->probe_class == kc), cap(cap_) {
+    if (on && cap) {
+      if (!e->pstamp || *cap >= kStampSites) { on = false; return; }
+      idx = (size_t)(*cap)++;
+      (void)stamp_begin(e->pstamp + 64 + idx, st);
+      return;
+    }
     if (on) {
       std::lock_guard<std::mutex> g(e->pm);
       if (e->ev_used + 2 > e->ev.size()) {
@@ -419,7 +471,11 @@ struct ProbeScope {
     }
   }
   ~ProbeScope() {
-    if (on) (void)hipEventRecord(e->ev[idx + 1], st);
+    if (!on) return;
+    if (cap)
+      (void)stamp_end(e->pstamp + 64 + idx, e->pstamp, st);
+    else
+      (void)hipEventRecord(e->ev[idx + 1], st);
   }
 };
 
@@ -429,6 +485,7 @@ struct Ctx {
   hipStream_t st;
   Bufs b;
   int B, N, nt, S, L, nfe, use_cfg, batch_mask;
+  int* cap_ev;  // non-null while capturing a step graph (probe stamp-site counter)
 };
 
 static GemmArgs gargs(const void* A, int64_t lda, const Lin& W, int M, void* C, int64_t ldc) {
@@ -517,8 +574,18 @@ static int prologue(Ctx& c, const float* t_host, int nt_vals, const float* cond,
   return 0;
 }
 
-// One packed cond/uncond backbone forward at table row k; result in b.p [S, L, mel].
-static int backbone_step(Ctx& c, int k) {
+// Copy the step's table row (k = *kstep) to the fixed per-step buffer the layers read.
+static int step_prep(Ctx& c) {
+  f5h_engine* e = c.e;
+  if (e->a.backbone == F5H_DIT)
+    KCK(step_begin(c.b.kstep, c.b.ada, e->ada.Npad, e->ada.Npad, c.b.ada_cur, c.st));
+  else
+    KCK(step_begin(c.b.kstep, c.b.temb, e->a.dim, e->a.dim, c.b.temb_cur, c.st));
+  return 0;
+}
+
+// One packed cond/uncond backbone forward for the current step; result in b.p [S, L, mel].
+static int backbone_step(Ctx& c) {
   f5h_engine* e = c.e;
   const f5h_arch& a = e->a;
   const int d = a.dim, bf = e->bf, H = a.heads, inner = H * 64;
@@ -548,7 +615,7 @@ static int backbone_step(Ctx& c, int k) {
     cv.mode = 0;
     cv.y = b.c1;
     {
-      ProbeScope ps(e, KC_CONV, st);
+      ProbeScope ps(e, KC_CONV, st, c.cap_ev);
       KCK(conv_pos(bf, cv, st));
     }
     cv.x = b.c1;
@@ -562,9 +629,9 @@ static int backbone_step(Ctx& c, int k) {
     cv.resid = b.h0;
     KCK(conv_pos(bf, cv, st));
   }
-  if (!dit) KCK(write_time_token(b.temb + (size_t)k * d, c.S, c.L, d, b.h, st));
+  if (!dit) KCK(write_time_token(b.temb_cur, c.S, c.L, d, b.h, st));
 
-  const float* ada_k = dit ? b.ada + (size_t)k * e->ada.Npad : nullptr;
+  const float* ada_k = dit ? b.ada_cur : nullptr;
   float* h = b.h;
   float* h2 = b.h2;
   for (int l = 0; l < a.depth; ++l) {
@@ -597,7 +664,7 @@ static int backbone_step(Ctx& c, int k) {
       g.k = b.k;
       g.v = b.v;
       g.q_scale = 0.125f * 1.4426950408889634f;  // softmax scale 1/sqrt(64) in log2 units, folded into q
-      ProbeScope ps(e, KC_QKV, st);
+      ProbeScope ps(e, KC_QKV, st, c.cap_ev);
       KCK(gemm(bf, EPI_QKV, g, st));
     }
     {
@@ -612,18 +679,18 @@ static int backbone_step(Ctx& c, int k) {
       at.kv_len = (a.attn_mask_enabled && c.batch_mask) ? b.kvlen : nullptr;
       at.scale = 0.125f;
       at.prescaled = 1;
-      ProbeScope ps(e, KC_ATTN, st);
+      ProbeScope ps(e, KC_ATTN, st, c.cap_ev);
       KCK(attention(bf, at, st));
     }
     {
       GemmArgs g = gargs(b.o, inner, Ly.out, rows, h, d);
       g.gate = ad ? ad + 2 * d : nullptr;  // gate_msa
       g.rowkeep = keep;                    // masked_fill of pad rows (modules.py:552-554)
-      ProbeScope ps(e, KC_OUT, st);
+      ProbeScope ps(e, KC_OUT, st, c.cap_ev);
       KCK(gemm(bf, EPI_RESID, g, st));
     }
     {
-      ProbeScope ps(e, KC_NORM, st);
+      ProbeScope ps(e, KC_NORM, st, c.cap_ev);
       if (dit)
         KCK(ln_modulate(bf, h, rows, d, ad + 3 * d /*shift_mlp*/, ad + 4 * d /*scale_mlp*/, b.aop, st));
       else
@@ -631,13 +698,13 @@ static int backbone_step(Ctx& c, int k) {
     }
     {
       GemmArgs g = gargs(b.aop, d, Ly.ff1, rows, b.f, a.ff_dim);
-      ProbeScope ps(e, KC_FFN1, st);
+      ProbeScope ps(e, KC_FFN1, st, c.cap_ev);
       KCK(gemm(bf, EPI_GELU_TANH, g, st));
     }
     {
       GemmArgs g = gargs(b.f, a.ff_dim, Ly.ff2, rows, h, d);
       g.gate = ad ? ad + 5 * d : nullptr;  // gate_mlp
-      ProbeScope ps(e, KC_FFN2, st);
+      ProbeScope ps(e, KC_FFN2, st, c.cap_ev);
       KCK(gemm(bf, EPI_RESID, g, st));
     }
   }
@@ -685,6 +752,7 @@ int f5h_engine_create(const f5h_arch* arch, const f5h_weight* weights, int32_t n
   e->bf = arch->compute == F5H_BF16;
   e->esz = e->bf ? 2 : 4;
   e->tdp = (arch->text_dim + 63) / 64 * 64;
+  if (const char* gv = getenv("F5H_GRAPH")) e->graph_mode = atoi(gv) ? 1 : 0;
   WMap W;
   for (int i = 0; i < n_weights; ++i) W.m[weights[i].name] = {weights[i].data, weights[i].numel};
   int rc = pack_all(e, W);
@@ -692,12 +760,27 @@ int f5h_engine_create(const f5h_arch* arch, const f5h_weight* weights, int32_t n
     f5h_engine_destroy(e);
     return rc;
   }
+  {
+    void* p = nullptr;
+    int khz = 0;
+    if (hipMalloc(&p, 4096 * sizeof(unsigned long long)) != hipSuccess ||
+        hipMemset(p, 0, 4096 * sizeof(unsigned long long)) != hipSuccess) {
+      if (p) (void)hipFree(p);
+      f5h_engine_destroy(e);
+      return fail(F5H_EHIP, "probe stamp buffer");
+    }
+    e->allocs.push_back(p);
+    e->pstamp = reinterpret_cast<unsigned long long*>(p);
+    if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, device) == hipSuccess) e->wall_khz = khz;
+  }
   *out = e;
   return 0;
 }
 
 void f5h_engine_destroy(f5h_engine* e) {
   if (!e) return;
+  for (GraphEntry* g : e->graphs) graph_entry_free(g);
+  if (e->cap) (void)hipStreamDestroy(e->cap);
   for (void* p : e->allocs) (void)hipFree(p);
   for (auto x : e->ev) (void)hipEventDestroy(x);
   delete e;
@@ -723,6 +806,8 @@ static int check_ws(f5h_engine* e, int B, int N, int nfe, int use_cfg, void* w, 
   return 0;
 }
 
+static int run_steps(Ctx& c, const f5h_sample_args* a, const void* ws);
+
 int f5h_sample(f5h_engine* e, void* stream, const f5h_sample_args* a, void* workspace, size_t workspace_bytes) {
   if (!e || !a) return fail(F5H_EINVAL, "null engine/args");
   if (a->B <= 0 || a->N <= 0 || a->nt < 0 || a->nfe <= 0 || a->nfe > 512)
@@ -746,14 +831,27 @@ int f5h_sample(f5h_engine* e, void* stream, const f5h_sample_args* a, void* work
   // the ODE evaluates fn at t_0 .. t_{nfe-1}
   RC(prologue(c, a->t_grid, c.nfe, a->cond, a->cond_mask, a->text, a->duration));
   const size_t ysz = (size_t)c.B * c.N * e->a.mel_dim;
-  HIPCK(hipMemcpyAsync(a->out, a->y0, ysz * sizeof(float), hipMemcpyDeviceToDevice, c.st));
+  HIPCK(hipMemcpyAsync(c.b.y, a->y0, ysz * sizeof(float), hipMemcpyDeviceToDevice, c.st));
   if (a->trajectory)
     HIPCK(hipMemcpyAsync(a->trajectory, a->y0, ysz * sizeof(float), hipMemcpyDeviceToDevice, c.st));
-  HIPCK(pack_y(e->bf, a->out, c.B * c.N, e->a.mel_dim, c.b.ypad, c.st));
-  for (int k = 0; k < c.nfe; ++k) {
-    RC(backbone_step(c, k));
+  HIPCK(pack_y(e->bf, c.b.y, c.B * c.N, e->a.mel_dim, c.b.ypad, c.st));
+  HIPCK(grid_upload(a->t_grid, c.nfe + 1, c.b.tgrid, c.st));
+  HIPCK(ptr_upload(a->trajectory, c.b.trajp, c.st));
+  HIPCK(hipMemsetAsync(c.b.kstep, 0, sizeof(int), c.st));
+  RC(run_steps(c, a, workspace));
+  HIPCK(final_where_out(a->cond, a->cond_mask, c.b.y, a->out, c.B, c.N, e->a.mel_dim, c.st));
+  return 0;
+}
+
+// Reference-equivalent eager form of the old loop body, kept as the graph's capture source:
+// step_prep -> backbone -> CFG + Euler (dt and trajectory slot from the device step index) -> k++.
+static int enqueue_step(Ctx& c, const f5h_sample_args* a) {
+  f5h_engine* e = c.e;
+  {
+    RC(step_prep(c));
+    RC(backbone_step(c));
     EulerArgs u{};
-    u.y = a->out;
+    u.y = c.b.y;
     u.B = c.B;
     u.N = c.N;
     u.mel = e->a.mel_dim;
@@ -763,13 +861,87 @@ int f5h_sample(f5h_engine* e, void* stream, const f5h_sample_args* a, void* work
     u.p_ld = e->a.mel_dim;
     u.use_cfg = c.use_cfg;
     u.cfg = a->cfg_strength;
-    u.dt = a->t_grid[k + 1] - a->t_grid[k];
+    u.dt = 0.f;
+    u.kstep = c.b.kstep;
+    u.tgrid = c.b.tgrid;
     u.ypad = c.b.ypad;
     u.compute = e->bf;
-    u.traj = a->trajectory ? a->trajectory + (size_t)(k + 1) * ysz : nullptr;
-    HIPCK(cfg_euler(u, c.st));
+    u.traj = nullptr;
+    u.trajp = c.b.trajp;
+    KCK(cfg_euler(u, c.st));
+    KCK(step_advance(c.b.kstep, c.st));
   }
-  HIPCK(final_where(a->cond, a->cond_mask, a->out, c.B, c.N, e->a.mel_dim, c.st));
+  return 0;
+}
+
+// The NFE loop: eager launches, or one captured step graph replayed nfe times.
+static int run_steps(Ctx& c, const f5h_sample_args* a, const void* ws) {
+  f5h_engine* e = c.e;
+  if (!e->graph_mode) {
+    for (int k = 0; k < c.nfe; ++k) RC(enqueue_step(c, a));
+    return 0;
+  }
+  GraphKey key{};
+  key.ws = ws;
+  key.B = c.B;
+  key.N = c.N;
+  key.nfe = c.nfe;
+  key.use_cfg = c.use_cfg;
+  key.batch_mask = c.batch_mask;
+  key.probe = e->probe_class;
+  std::memcpy(&key.cfg_bits, &a->cfg_strength, 4);
+  hipGraphExec_t exec = nullptr;
+  {
+    std::lock_guard<std::mutex> g(e->gm);
+    GraphEntry* hit = nullptr;
+    for (GraphEntry* x : e->graphs)
+      if (x->key == key) hit = x;
+    if (!hit) {
+      if (!e->cap) HIPCK(hipStreamCreateWithFlags(&e->cap, hipStreamNonBlocking));
+      GraphEntry* ne = new GraphEntry();
+      ne->key = key;
+      Ctx cc = c;
+      cc.st = e->cap;
+      int sites = 0;
+      cc.cap_ev = &sites;
+      hipError_t be = hipStreamBeginCapture(e->cap, hipStreamCaptureModeThreadLocal);
+      if (be != hipSuccess) {
+        graph_entry_free(ne);
+        return fail(F5H_EHIP, std::string("hipStreamBeginCapture: ") + hipGetErrorString(be));
+      }
+      const int rc = enqueue_step(cc, a);
+      hipGraph_t graph = nullptr;
+      const hipError_t ce = hipStreamEndCapture(e->cap, &graph);
+      if (rc || ce != hipSuccess) {
+        if (graph) (void)hipGraphDestroy(graph);
+        graph_entry_free(ne);
+        if (rc) return rc;
+        return fail(F5H_EHIP, std::string("hipStreamEndCapture: ") + hipGetErrorString(ce));
+      }
+      const hipError_t ie = hipGraphInstantiate(&ne->exec, graph, nullptr, nullptr, 0);
+      (void)hipGraphDestroy(graph);
+      if (ie != hipSuccess) {
+        ne->exec = nullptr;
+        graph_entry_free(ne);
+        return fail(F5H_EHIP, std::string("hipGraphInstantiate: ") + hipGetErrorString(ie));
+      }
+      if (e->graphs.size() >= 8) {  // evict the least recently used step graph
+        (void)hipDeviceSynchronize();  // it may still be in flight on another stream
+        size_t lru = 0;
+        for (size_t i = 1; i < e->graphs.size(); ++i)
+          if (e->graphs[i]->stamp < e->graphs[lru]->stamp) lru = i;
+        graph_entry_free(e->graphs[lru]);
+        e->graphs.erase(e->graphs.begin() + lru);
+      }
+      e->graphs.push_back(ne);
+      e->n_captures++;
+      hit = ne;
+    }
+    hit->stamp = ++e->use_ctr;
+    exec = hit->exec;
+    e->n_replays += c.nfe;
+  }
+  for (int k = 0; k < c.nfe; ++k) HIPCK(hipGraphLaunch(exec, c.st));
   return 0;
 }
 
@@ -794,7 +966,9 @@ int f5h_forward(f5h_engine* e, void* stream, const f5h_forward_args* a, void* wo
   float tg[2] = {a->t, a->t};
   RC(prologue(c, tg, 1, a->cond, a->cond_mask, a->text, a->duration));
   HIPCK(pack_y(e->bf, a->x, c.B * c.N, e->a.mel_dim, c.b.ypad, c.st));
-  RC(backbone_step(c, 0));
+  HIPCK(hipMemsetAsync(c.b.kstep, 0, sizeof(int), c.st));
+  RC(step_prep(c));
+  RC(backbone_step(c));
   HIPCK(copy_pred(c.b.p, c.S, c.L, e->a.backbone == F5H_DIT ? 0 : 1, e->a.mel_dim, e->a.mel_dim, a->pred, c.st));
   return 0;
 }
@@ -806,6 +980,7 @@ int f5h_probe_enable(f5h_engine* e, int32_t kclass, int32_t enable) {
   e->ev_used = 0;
   e->probe_launches = 0;
   e->probe_ms = 0.0;
+  if (e->pstamp) HIPCK(hipMemset(e->pstamp, 0, 2 * sizeof(unsigned long long)));
   return 0;
 }
 
@@ -819,8 +994,35 @@ int f5h_probe_read(f5h_engine* e, int64_t* launches, double* total_ms) {
     HIPCK(hipEventElapsedTime(&t, e->ev[i], e->ev[i + 1]));
     ms += t;
   }
-  if (launches) *launches = (int64_t)(e->ev_used / 2);
+  int64_t n = (int64_t)(e->ev_used / 2);
+  // step graphs: launches timed by device wall-clock stamps, accumulated on the device
+  if (e->pstamp && e->wall_khz > 0.0) {
+    HIPCK(hipSetDevice(e->dev));
+    HIPCK(hipDeviceSynchronize());
+    unsigned long long acc[2] = {0, 0};
+    HIPCK(hipMemcpy(acc, e->pstamp, sizeof(acc), hipMemcpyDeviceToHost));
+    ms += (double)acc[0] / e->wall_khz;
+    n += (int64_t)acc[1];
+  }
+  if (launches) *launches = n;
   if (total_ms) *total_ms = ms;
+  return 0;
+}
+
+int f5h_set_graph_mode(f5h_engine* e, int32_t mode) {
+  if (!e) return fail(F5H_EINVAL, "null engine");
+  if (mode != 0 && mode != 1) return fail(F5H_EINVAL, "graph mode must be 0 (eager) or 1 (step graph)");
+  std::lock_guard<std::mutex> g(e->gm);
+  e->graph_mode = mode;
+  return 0;
+}
+
+int f5h_graph_stats(f5h_engine* e, int64_t* captures, int64_t* replays, int32_t* cached) {
+  if (!e) return fail(F5H_EINVAL, "null engine");
+  std::lock_guard<std::mutex> g(e->gm);
+  if (captures) *captures = e->n_captures;
+  if (replays) *replays = e->n_replays;
+  if (cached) *cached = (int32_t)e->graphs.size();
   return 0;
 }
 

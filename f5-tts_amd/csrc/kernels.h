@@ -104,10 +104,27 @@ struct EulerArgs {
   int use_cfg; float cfg; float dt;
   void* ypad; int compute;      // refreshed operand copy (or null)
   float* traj;                  // [B,N,mel] slot to copy y into (or null)
+  // device-indexed form (graph replay): when kstep is set, dt = tgrid[k+1] - tgrid[k] and the
+  // trajectory slot is traj + (k+1)*B*N*mel, k = *kstep (dt above is ignored)
+  // trajectory base (or null) read from *trajp in the device-indexed form
+  const int* kstep; const float* tgrid; float* const* trajp;
 };
 hipError_t cfg_euler(const EulerArgs& a, hipStream_t st);
+// host grid t[n <= 512] -> device (by kernel argument)
+hipError_t grid_upload(const float* t_host, int n, float* out, hipStream_t st);
+// dst[0..n) = src[k*stride ..], k = *kstep (n, stride multiples of 4)
+hipError_t step_begin(const int* kstep, const float* src, int64_t stride, int n, float* dst, hipStream_t st);
+// probe stamps: *slot = wall clock; acc[0] += now - *slot, acc[1] += 1
+hipError_t stamp_begin(unsigned long long* slot, hipStream_t st);
+hipError_t stamp_end(const unsigned long long* slot, unsigned long long* acc, hipStream_t st);
+// *kstep += 1
+hipError_t step_advance(int* kstep, hipStream_t st);
 hipError_t final_where(const float* cond, const uint8_t* cond_mask, float* y, int B, int N, int mel,
                        hipStream_t st);
+hipError_t final_where_out(const float* cond, const uint8_t* cond_mask, const float* y, float* out, int B, int N,
+                           int mel, hipStream_t st);
+// *slot = p (stream-ordered)
+hipError_t ptr_upload(float* p, float** slot, hipStream_t st);
 // rowkeep[s*L + pos] = (pos - off < dur[s % B]) || pos < off ; for S sequences
 hipError_t build_rowkeep(const int32_t* dur, int B, int S, int L, int off, uint8_t* keep, hipStream_t st);
 // kv_len[s] = dur[s % B] + off

@@ -30,6 +30,8 @@ EXPORTS = (
     "f5h_forward",
     "f5h_probe_enable",
     "f5h_probe_read",
+    "f5h_set_graph_mode",
+    "f5h_graph_stats",
     "f5h_op_linear",
     "f5h_op_attention",
     "f5h_gemm_force_config",
@@ -102,6 +104,10 @@ def lib():
     L.f5h_probe_enable.restype = ctypes.c_int
     L.f5h_probe_read.argtypes = [vp, ctypes.POINTER(i64), ctypes.POINTER(ctypes.c_double)]
     L.f5h_probe_read.restype = ctypes.c_int
+    L.f5h_set_graph_mode.argtypes = [vp, i32]
+    L.f5h_set_graph_mode.restype = ctypes.c_int
+    L.f5h_graph_stats.argtypes = [vp, ctypes.POINTER(i64), ctypes.POINTER(i64), ctypes.POINTER(i32)]
+    L.f5h_graph_stats.restype = ctypes.c_int
     L.f5h_op_linear.argtypes = [vp, i32, i32, i32, i32, vp, vp, vp, vp, vp, sz]
     L.f5h_op_linear.restype = ctypes.c_int
     L.f5h_op_attention.argtypes = [vp, i32, i32, i32, i32, vp, vp, vp, vp, i32, vp, vp, sz]

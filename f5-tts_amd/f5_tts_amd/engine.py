@@ -65,6 +65,11 @@ class Engine:
                        "f5h_engine_create")
         self._h = h
         self._lock = threading.Lock()
+        # per-(stream, size) workspaces kept across calls: the engine's NFE-step hipGraph is keyed
+        # by the workspace address, so a stable workspace makes every call after the first a replay.
+        # A call holds its workspace's lock while it enqueues, so calls sharing a stream serialise
+        # in stream order and calls on different streams never share a workspace.
+        self._ws_cache: dict = {}
 
     def __del__(self):
         h = getattr(self, "_h", None)
@@ -81,6 +86,26 @@ class Engine:
 
     def _workspace(self, nbytes):
         return torch.empty(max(nbytes, 256), dtype=torch.uint8, device=self.device)
+
+    def _cached_workspace(self, nbytes, stream):
+        with self._lock:
+            ent = self._ws_cache.get((stream, nbytes))
+            if ent is None:
+                if len(self._ws_cache) >= 4:
+                    self._ws_cache.pop(next(iter(self._ws_cache)))
+                ent = (self._workspace(nbytes), threading.Lock())
+                self._ws_cache[(stream, nbytes)] = ent
+            return ent
+
+    def set_graph_mode(self, on: bool):
+        """True: the NFE loop replays one captured hipGraph step (default); False: eager launches."""
+        _lib.check(_lib.lib().f5h_set_graph_mode(self._h, int(bool(on))), "set_graph_mode")
+
+    def graph_stats(self):
+        cap, rep, n = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int32()
+        _lib.check(_lib.lib().f5h_graph_stats(self._h, ctypes.byref(cap), ctypes.byref(rep), ctypes.byref(n)),
+                   "graph_stats")
+        return {"captures": cap.value, "replays": rep.value, "cached": n.value}
 
     # ------------------------------------------------------------------ calls
     def sample(self, cond, cond_mask, text, duration, y0, t_grid, cfg_strength, use_batch_mask,
@@ -103,7 +128,11 @@ class Engine:
                 if keep_trajectory else None)
         use_cfg = cfg_strength >= 1e-5
         need = self.workspace_bytes(B, N, nt, nfe, use_cfg)
-        ws = workspace if workspace is not None and workspace.numel() >= need else self._workspace(need)
+        stream = _lib.stream_handle(self.device)
+        if workspace is not None and workspace.numel() >= need:
+            ws, wlock = workspace, threading.Lock()
+        else:
+            ws, wlock = self._cached_workspace(need, stream)
         a = _lib.SampleArgs()
         a.B, a.N, a.nt, a.nfe = B, N, nt, nfe
         a.cond, a.cond_mask, a.text, a.duration, a.y0 = (cond.data_ptr(), cmask.data_ptr(), text.data_ptr(),
@@ -113,9 +142,9 @@ class Engine:
         a.use_batch_mask = int(bool(use_batch_mask))
         a.out = out.data_ptr()
         a.trajectory = traj.data_ptr() if traj is not None else None
-        with torch.cuda.device(self.device):
-            _lib.check(_lib.lib().f5h_sample(self._h, _lib.stream_handle(self.device), ctypes.byref(a),
-                                             ws.data_ptr(), ws.numel()), "f5h_sample")
+        with torch.cuda.device(self.device), wlock:
+            _lib.check(_lib.lib().f5h_sample(self._h, stream, ctypes.byref(a), ws.data_ptr(), ws.numel()),
+                       "f5h_sample")
         return out, traj
 
     def forward(self, x, cond, cond_mask, text, duration, t: float, use_batch_mask):

@@ -127,6 +127,15 @@ int f5h_forward(f5h_engine* eng, void* stream, const f5h_forward_args* args, voi
 int f5h_probe_enable(f5h_engine* eng, int32_t kclass, int32_t enable);
 int f5h_probe_read(f5h_engine* eng, int64_t* launches, double* total_ms);
 
+/* NFE-step graph (the CFM.sample ODE loop, cfm.py:218 -> torchdiffeq Euler): with mode 1 (default;
+ * env F5H_GRAPH=0 selects 0 at engine creation) f5h_sample captures one NFE step -- table-row
+ * copy, backbone forward, CFG combine + Euler update, device step counter -- into a hipGraph on
+ * first use for a (workspace, out, trajectory, B, N, nfe, cfg, mask, probe) key and replays it
+ * nfe times; mode 0 launches the same sequence eagerly. Results are bitwise identical.
+ * f5h_graph_stats: captures so far, step replays so far, graphs cached (LRU, at most 8). */
+int f5h_set_graph_mode(f5h_engine* eng, int32_t mode);
+int f5h_graph_stats(f5h_engine* eng, int64_t* captures, int64_t* replays, int32_t* cached);
+
 /* Op-level entry points (parity tests / microbenchmarks). Device pointers, row-major. */
 /* C[M,N] = A[M,K] . W[N,K]^T + bias  (fp32 in/out; compute = F5H_FP32 or F5H_BF16 operands) */
 int f5h_op_linear(void* stream, int32_t compute, int32_t M, int32_t N, int32_t K, const float* A,

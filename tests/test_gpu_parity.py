@@ -273,3 +273,44 @@ def test_batch_permutation_equivariance_at_c3_shape(masked):
     for i in range(c3["B"]):
         L = int(inp["lens"][i])
         assert torch.equal(out[i, :L].cpu(), inp["cond"][i, :L])
+
+
+@pytest.mark.parametrize("name", ["dit_tiny_sample_b3", "dit_tiny_sample_b3_masked", "unett_tiny_sample_b3"])
+def test_step_graph_bitwise_equals_eager(name):
+    """The hipGraph-replayed NFE step (default) and the eager launch sequence give bitwise
+    identical outputs and trajectories; the second call on the same shape replays the cached
+    graph (no new capture), and a different cfg strength captures its own graph."""
+    _need_gpu()
+    if name not in gc.SAMPLE_CASES:
+        pytest.skip(f"{name} not a sample case")
+    tag, spec, nfe, sway, cfg = gc.SAMPLE_CASES[name]
+    arch = gc.arch_of(tag)
+    m = _model(arch, "bf16")
+    inp = synthetic.make_case(**spec)
+    dur = torch.maximum(torch.maximum((inp["text"] != -1).sum(-1), inp["lens"]) + 1, inp["duration"])
+    y0 = synthetic.reference_noise(dur, gc.SEED)
+    eng = m.transformer.get_engine("bf16", m.device)
+
+    def run(cfg_strength=cfg):
+        out, traj = m.sample(cond=inp["cond"].to(DEV), text=inp["text"].to(DEV), duration=inp["duration"].to(DEV),
+                             lens=inp["lens"].to(DEV), steps=nfe, cfg_strength=cfg_strength,
+                             sway_sampling_coef=sway, y0=y0.to(DEV), keep_trajectory=True)
+        torch.cuda.synchronize()
+        return out.clone(), traj.clone()
+
+    eng.set_graph_mode(False)
+    o_e, t_e = run()
+    eng.set_graph_mode(True)
+    s0 = eng.graph_stats()
+    o_g, t_g = run()
+    s1 = eng.graph_stats()
+    o_g2, t_g2 = run()
+    s2 = eng.graph_stats()
+    assert torch.equal(o_g, o_e) and torch.equal(t_g, t_e)
+    assert torch.equal(o_g2, o_e) and torch.equal(t_g2, t_e)
+    assert s1["captures"] == s0["captures"] + 1
+    assert s2["captures"] == s1["captures"], "second call on the same shape must replay"
+    assert s2["replays"] - s1["replays"] == t_e.shape[0] - 1
+    o_c, _ = run(cfg_strength=cfg + 0.5)
+    assert eng.graph_stats()["captures"] == s2["captures"] + 1
+    assert not torch.equal(o_c, o_e)
