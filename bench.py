@@ -117,7 +117,7 @@ def main():
     ap.add_argument("--preset", default="F5TTS_v1_Base")
     ap.add_argument("--compute", default="bf16")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--probe", default="attention", help="kernel class timed with HIP events for the roofline")
+    ap.add_argument("--probe", default="attention", help="kernel class timed live (in-kernel device wall-clock stamps) for the roofline")
     ap.add_argument("--config", default="c2", choices=("c2", "c3", "c5"),
                     help="workload (SURVEY §8d); c2 is the headline line")
     ap.add_argument("--probe-all", action="store_true",
@@ -197,7 +197,9 @@ def main():
         roof = {"bound": "mfma", "kernel": args.probe, "achieved": round(ach, 2), "peak": PEAK_BF16_TFLOPS,
                 "unit": "TFLOP/s", "frac": round(ach / PEAK_BF16_TFLOPS, 4), "traffic": traffic,
                 "traffic_unit": "bytes/launch", "traffic_source": tsrc,
-                "avg_launch_ms": round(avg_ms, 5), "launches": n_launch, "flops_per_launch": fl}
+                "avg_launch_ms": round(avg_ms, 5), "launches": n_launch, "flops_per_launch": fl,
+                "timing": "in-kernel s_memrealtime stamps: first workgroup start to last wave end of the probed "
+                          "kernel's launches in every 4th ODE step inside the timed region (all layers)"}
 
     if args.probe_all and rank == 0:
         import sys
@@ -211,7 +213,7 @@ def main():
             if n:
                 avg = ms / n
                 fl = class_flops(kc, arch, S, L)
-                print(f"[probe] {kc:9s} launches/call {n // max(1, min(args.steps, 3)):4d}  avg {avg * 1e3:8.2f} us"
+                print(f"[probe] {kc:9s} sampled launches {n:5d}  avg {avg * 1e3:8.2f} us"
                       + (f"  {fl / (avg * 1e-3) / 1e12:7.1f} TF/s" if fl else ""), file=sys.stderr, flush=True)
 
     cpu = None

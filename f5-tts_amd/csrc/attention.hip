@@ -55,6 +55,7 @@ F5H_DEV void attn_block(int& qb, int& bh) {
 
 template <bool PRESCALED, int DBG>
 __global__ __launch_bounds__(256, 2) void attn_bf16_kernel(AttnArgs a) {
+  const ProbeT probe_t = probe_enter(a.probe);
   constexpr int TILE_B = 2 * 64 * 128;  // K + V tile bytes (64 keys x 64 dh bf16 each)
   constexpr int NS = 3;                 // LDS ring: one tile read while two are in flight
   constexpr int DPS = 4;                // DMA instructions per tile per wave (K 2 + V 2)
@@ -297,6 +298,7 @@ __global__ __launch_bounds__(256, 2) void attn_bf16_kernel(AttnArgs a) {
         *reinterpret_cast<bf16x4*>(O + 32 * u + 8 * r4 + 4 * h) = w;
       }
   }
+  probe_exit(a.probe, probe_t);
 }
 
 // ---------------------------------------------------------------- bf16 kernel, v2
@@ -313,6 +315,7 @@ __global__ __launch_bounds__(256, 2) void attn_bf16_kernel(AttnArgs a) {
 //     K/V tiles of 64 keys by LDS-DMA into a 3-deep ring shared by all waves.
 template <bool PRESCALED, int NW>
 __global__ __launch_bounds__(64 * NW, 1) void attn_bf16_v2_kernel(AttnArgs a) {
+  const ProbeT probe_t = probe_enter(a.probe);
   constexpr int TILE_B = 2 * 64 * 128;  // K + V tile bytes (64 keys x 64 dh bf16 each)
   constexpr int NS = 3;
   constexpr int CPW = 512 / (64 * NW);  // 16-B chunks of one K (or V) tile per lane
@@ -535,6 +538,7 @@ __global__ __launch_bounds__(64 * NW, 1) void attn_bf16_v2_kernel(AttnArgs a) {
         *reinterpret_cast<bf16x4*>(O + 32 * u + 8 * r4 + 4 * h) = w;
       }
   }
+  probe_exit(a.probe, probe_t);
 }
 
 // ---------------------------------------------------------------- bf16 kernel, v3 (ping-pong)
@@ -550,6 +554,7 @@ __global__ __launch_bounds__(64 * NW, 1) void attn_bf16_v2_kernel(AttnArgs a) {
 // read (group 1, V-half t, half-period 2t+2) is retired (lgkmcnt(0)) before the barrier ending it.
 template <bool PRESCALED>
 __global__ __launch_bounds__(512, 1) void attn_bf16_v3_kernel(AttnArgs a) {
+  const ProbeT probe_t = probe_enter(a.probe);
   constexpr int NW = 8;
   constexpr int TILE_B = 2 * 64 * 128;
   constexpr int NS = 4;
@@ -787,6 +792,7 @@ __global__ __launch_bounds__(512, 1) void attn_bf16_v3_kernel(AttnArgs a) {
         *reinterpret_cast<bf16x4*>(O + 32 * u + 8 * r4 + 4 * h) = w;
       }
   }
+  probe_exit(a.probe, probe_t);
 }
 
 // ---------------------------------------------------------------- bf16 kernel, v4 (fixed offset)
@@ -823,6 +829,7 @@ F5H_DEV void attn_row_exact(const AttnArgs& a, const bf16* Q, const bf16* K, con
 
 template <bool PRESCALED>
 __global__ __launch_bounds__(512, 1) void attn_bf16_v4_kernel(AttnArgs a) {
+  const ProbeT probe_t = probe_enter(a.probe);
   constexpr int NW = 8;
   constexpr int TILE_B = 2 * 64 * 128;
   constexpr int NS = 4;
@@ -1059,12 +1066,14 @@ __global__ __launch_bounds__(512, 1) void attn_bf16_v4_kernel(AttnArgs a) {
         *reinterpret_cast<bf16x4*>(O + 32 * u + 8 * r4 + 4 * h) = w;
       }
   }
+  probe_exit(a.probe, probe_t);
 }
 
 __device__ uint64_t g_attn_stamps[4 * 8 * 8];
 
 template <bool PRESCALED, bool STAMP = false>
 __global__ __launch_bounds__(512, 1) void attn_bf16_v5_kernel(AttnArgs a) {
+  const ProbeT probe_t = probe_enter(a.probe);
   uint64_t st_acc[6] = {0, 0, 0, 0, 0, 0}, st_prev = 0;
   // diagnostic build only: cycles per segment of the K loop, summed (s_memtime drains lgkmcnt)
   auto stamp = [&](int seg) {
@@ -1349,10 +1358,12 @@ __global__ __launch_bounds__(512, 1) void attn_bf16_v5_kernel(AttnArgs a) {
         *reinterpret_cast<bf16x4*>(O + 32 * u + 8 * r4 + 4 * h) = w;
       }
   }
+  probe_exit(a.probe, probe_t);
 }
 
 template <bool PRESCALED, bool STAMP = false>
 __global__ __launch_bounds__(512, 1) void attn_bf16_v6_kernel(AttnArgs a) {
+  const ProbeT probe_t = probe_enter(a.probe);
   uint64_t st_acc[6] = {0, 0, 0, 0, 0, 0}, st_prev = 0;
   // diagnostic build only: cycles per segment of the K loop, summed (s_memtime drains lgkmcnt)
   auto stamp = [&](int seg) {
@@ -1658,6 +1669,7 @@ __global__ __launch_bounds__(512, 1) void attn_bf16_v6_kernel(AttnArgs a) {
         *reinterpret_cast<bf16x4*>(O + 32 * u + 8 * r4 + 4 * h) = w;
       }
   }
+  probe_exit(a.probe, probe_t);
 }
 
 // ---------------------------------------------------------------- bf16 kernel, v7
@@ -1677,6 +1689,7 @@ __global__ __launch_bounds__(512, 1) void attn_bf16_v6_kernel(AttnArgs a) {
 // last reads (V_j, iteration j-1) retired at the end of iteration j-1.
 template <bool PRESCALED>
 __global__ __launch_bounds__(256, 1) void attn_bf16_v7_kernel(AttnArgs a) {
+  const ProbeT probe_t = probe_enter(a.probe);
   constexpr int NW = 4;
   constexpr int TILE_B = 2 * 64 * 128;
   constexpr int NS = 4;
@@ -2011,10 +2024,12 @@ __global__ __launch_bounds__(256, 1) void attn_bf16_v7_kernel(AttnArgs a) {
       }
     }
   }
+  probe_exit(a.probe, probe_t);
 }
 
 // ---------------------------------------------------------------- fp32 parity kernel
 __global__ __launch_bounds__(64) void attn_f32_kernel(AttnArgs a) {
+  const ProbeT probe_t = probe_enter(a.probe);
   __shared__ float Ks[32][65];
   __shared__ float Vs[32][64];
   const int lane = threadIdx.x;
@@ -2072,6 +2087,7 @@ __global__ __launch_bounds__(64) void attn_f32_kernel(AttnArgs a) {
 #pragma unroll
     for (int d = 0; d < 64; ++d) O[d] = o[d] * inv;
   }
+  probe_exit(a.probe, probe_t);
 }
 
 static int g_attn_variant = -1;

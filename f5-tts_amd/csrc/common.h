@@ -5,6 +5,8 @@
 
 #include <type_traits>
 
+#include "kernels.h"
+
 typedef __bf16 bf16;
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
@@ -32,6 +34,46 @@ F5H_DEV float gelu_tanh(float x) {  // nn.GELU(approximate="tanh"), modules.py:3
   float u = k0 * (x + k1 * x * x * x);
   return 0.5f * x * (1.f + tanhf(u));
 }
+// bf16-mode form: 0.5x(1+tanh(u)) == x * sigmoid(2u) = x / (1 + 2^(-2u*log2 e)); v_exp_f32 + v_rcp_f32
+// (rel. error ~1e-6, far below the bf16 rounding of the result; the fp32 parity mode keeps tanhf)
+F5H_DEV float gelu_tanh_fast(float x) {
+  const float k0 = 0.7978845608028654f * 2.f * 1.4426950408889634f, k1 = 0.044715f;
+  const float u = k0 * (x + k1 * x * x * x);
+  return x * __builtin_amdgcn_rcpf(1.f + __builtin_amdgcn_exp2f(-u));
+}
+// ---------------------------------------------------------------- in-kernel launch probe
+// Kernel-side timing of probed launches (f5h_probe_*): the first thread of every workgroup
+// atomicMin's the device wall clock (s_memrealtime, 100 MHz) into start[tick] at entry and
+// every wave's lane 0 atomicMax's it into end[tick] at exit, so a launch's span is
+// max(end) - min(start) without extra launches or events in the stream (graph-replay safe).
+// slots = start row of this launch site; the end row is kProbeEnd entries further on.
+// (DevProbe, kProbeTicks/kProbeSites/kProbeEnd: kernels.h)
+F5H_DEV int64_t probe_slot(int k) {
+  return ((int64_t)k * f5h::kProbeLanes + (blockIdx.x & (f5h::kProbeLanes - 1))) * f5h::kProbeStride;
+}
+// Entry: wave 0 reads the clock into registers (wait retired at once, so no SMEM op stays in
+// flight under the kernels' hand-counted lgkmcnt waits) and loads the tick, consumed at exit.
+struct ProbeT {
+  unsigned long long t0;
+  int k;
+};
+F5H_DEV ProbeT probe_enter(const f5h::DevProbe& p) {
+  ProbeT r{0ull, -1};
+  if (p.slots) {
+    r.k = *p.tick;
+    r.t0 = wall_clock64();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  }
+  return r;
+}
+F5H_DEV void probe_exit(const f5h::DevProbe& p, const ProbeT& r) {
+  if (p.slots && (threadIdx.x & 63) == 0 && r.k >= 0 && r.k < f5h::kProbeTicks && r.k % f5h::kProbeEvery == 0) {
+    const int64_t i = probe_slot(r.k);
+    atomicMax(p.slots + f5h::kProbeEnd + i, (unsigned long long)wall_clock64());
+    if (threadIdx.x == 0) atomicMin(p.slots + i, r.t0);
+  }
+}
+
 F5H_DEV float gelu_erf(float x) {  // nn.GELU(), modules.py:266
   return 0.5f * x * (1.f + erff(x * 0.7071067811865476f));
 }

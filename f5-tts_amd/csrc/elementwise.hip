@@ -79,30 +79,33 @@ hipError_t step_begin(const int* kstep, const float* src, int64_t stride, int n,
   hipLaunchKernelGGL(step_begin_kernel, dim3(nblk(n / 4, 256)), dim3(256), 0, st, kstep, src, stride, n, dst);
   return hipGetLastError();
 }
-// Probe stamps (device wall clock, s_memrealtime) around a launch inside a step graph.
-__global__ void stamp_begin_kernel(unsigned long long* slot) {
-  if (threadIdx.x == 0) slot[0] = wall_clock64();
+// Probe stamps (device wall clock, s_memrealtime) around a launch that does not stamp itself:
+// same slot layout as the in-kernel probe (kernels.h).
+__global__ void stamp_begin_kernel(unsigned long long* slots, const int* tick) {
+  const int k = *tick;
+  if (threadIdx.x == 0 && k >= 0 && k < kProbeTicks && k % kProbeEvery == 0) atomicMin(slots + probe_slot(k), (unsigned long long)wall_clock64());
 }
-__global__ void stamp_end_kernel(const unsigned long long* slot, unsigned long long* acc) {
+__global__ void stamp_end_kernel(unsigned long long* slots, const int* tick) {
+  const int k = *tick;
+  if (threadIdx.x == 0 && k >= 0 && k < kProbeTicks && k % kProbeEvery == 0)
+    atomicMax(slots + kProbeEnd + probe_slot(k), (unsigned long long)wall_clock64());
+}
+hipError_t stamp_begin(unsigned long long* slots, const int* tick, hipStream_t st) {
+  hipLaunchKernelGGL(stamp_begin_kernel, dim3(1), dim3(64), 0, st, slots, tick);
+  return hipGetLastError();
+}
+hipError_t stamp_end(unsigned long long* slots, const int* tick, hipStream_t st) {
+  hipLaunchKernelGGL(stamp_end_kernel, dim3(1), dim3(64), 0, st, slots, tick);
+  return hipGetLastError();
+}
+__global__ void step_advance_kernel(int* kstep, int* tick) {
   if (threadIdx.x == 0) {
-    const unsigned long long t = wall_clock64();
-    atomicAdd(&acc[0], t - slot[0]);
-    atomicAdd(&acc[1], 1ull);
+    kstep[0] += 1;
+    tick[0] += 1;
   }
 }
-hipError_t stamp_begin(unsigned long long* slot, hipStream_t st) {
-  hipLaunchKernelGGL(stamp_begin_kernel, dim3(1), dim3(64), 0, st, slot);
-  return hipGetLastError();
-}
-hipError_t stamp_end(const unsigned long long* slot, unsigned long long* acc, hipStream_t st) {
-  hipLaunchKernelGGL(stamp_end_kernel, dim3(1), dim3(64), 0, st, slot, acc);
-  return hipGetLastError();
-}
-__global__ void step_advance_kernel(int* kstep) {
-  if (threadIdx.x == 0) kstep[0] += 1;
-}
-hipError_t step_advance(int* kstep, hipStream_t st) {
-  hipLaunchKernelGGL(step_advance_kernel, dim3(1), dim3(64), 0, st, kstep);
+hipError_t step_advance(int* kstep, int* tick, hipStream_t st) {
+  hipLaunchKernelGGL(step_advance_kernel, dim3(1), dim3(64), 0, st, kstep, tick);
   return hipGetLastError();
 }
 

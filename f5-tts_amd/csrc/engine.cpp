@@ -16,6 +16,8 @@
 
 #include <cmath>
 #include <cstring>
+#include <algorithm>
+#include <atomic>
 #include <mutex>
 #include <string>
 #include <unordered_map>
@@ -90,27 +92,33 @@ struct f5h_engine {
   uint64_t use_ctr = 0;
   int64_t n_captures = 0, n_replays = 0;
   // probe
+  // Probed launches are timed on the device wall clock (s_memrealtime): GEMM and attention
+  // kernels stamp themselves (DevProbe), the others get a stamp kernel on each side. Slots are
+  // indexed by (launch site within a step, device step tick), so eager launches and graph
+  // replays are timed alike. pstamp[0] (as int) = tick, bumped by every step; pslots =
+  // pstamp + 64: kProbeSites x kProbeTicks start stamps, then as many end stamps.
   std::mutex pm;
   int probe_class = -1;
-  std::vector<hipEvent_t> ev;  // pairs
-  size_t ev_used = 0;
-  int64_t probe_launches = 0;
-  double probe_ms = 0.0;
-  // graph-mode probe: device wall-clock stamps (s_memrealtime) around each probed launch;
-  // pstamp[0] = sum of ticks, pstamp[1] = launches, pstamp[64 + j] = start stamp of site j
   unsigned long long* pstamp = nullptr;
+  unsigned long long* pslots = nullptr;
+  int* ptick = nullptr;
   double wall_khz = 0.0;
 };
-static constexpr int kStampSites = 4096 - 64;
+static constexpr size_t kProbeBytes = (64 + 2 * (size_t)kProbeEnd) * sizeof(unsigned long long);
 
 // The step graph touches only workspace buffers (the ODE state, the trajectory base and the step
 // index live in the workspace), so it is keyed by the workspace and the launch shape alone.
+// Captured step graphs bake in the kernel choice: forcing a GEMM config or an attention variant
+// (tuning/tests) moves the epoch so that later calls capture afresh.
+static std::atomic<uint64_t> g_kernel_epoch{0};
+
 struct GraphKey {
   const void* ws;
   int B, N, nfe, use_cfg, batch_mask, probe;
+  uint64_t kernel_epoch;  // bumped whenever a forced GEMM config / attention variant changes
   uint32_t cfg_bits;
   bool operator==(const GraphKey& o) const {
-    return ws == o.ws && B == o.B && N == o.N && nfe == o.nfe &&
+    return ws == o.ws && B == o.B && N == o.N && nfe == o.nfe && kernel_epoch == o.kernel_epoch &&
            use_cfg == o.use_cfg && batch_mask == o.batch_mask && probe == o.probe && cfg_bits == o.cfg_bits;
   }
 };
@@ -438,44 +446,28 @@ static void layout(const f5h_engine* e, WS& ws, Bufs& b, int B, int N, int nfe, 
 
 // ---------------------------------------------------------------- probe
 enum { KC_FFN1 = 0, KC_ATTN = 1, KC_QKV = 2, KC_FFN2 = 3, KC_CONV = 4, KC_OUT = 5, KC_NORM = 6 };
+// Times one launch site when its kernel class is probed. With `kp` the kernel stamps itself
+// (GemmArgs/AttnArgs::probe); without, stamp kernels bracket the launch.
 struct ProbeScope {
   f5h_engine* e;
   hipStream_t st;
   bool on;
-  size_t idx = 0;
-  int* cap = nullptr;  // capturing a step graph: next stamp site (events cannot be timed in a graph)
-  ProbeScope(f5h_engine* e_, int kc, hipStream_t s, int* cap_ = nullptr)
-      : e(e_), st(s), on(e_->probe_class == kc), cap(cap_) {
-    if (on && cap) {
-      if (!e->pstamp || *cap >= kStampSites) { on = false; return; }
-      idx = (size_t)(*cap)++;
-      (void)stamp_begin(e->pstamp + 64 + idx, st);
-      return;
-    }
-    if (on) {
-      std::lock_guard<std::mutex> g(e->pm);
-      if (e->ev_used + 2 > e->ev.size()) {
-        for (int i = 0; i < 256; ++i) {
-          hipEvent_t x;
-          if (hipEventCreate(&x) != hipSuccess) break;
-          e->ev.push_back(x);
-        }
-      }
-      if (e->ev_used + 2 > e->ev.size()) {
-        on = false;
-        return;
-      }
-      idx = e->ev_used;
-      e->ev_used += 2;
-      (void)hipEventRecord(e->ev[idx], st);
+  bool self = false;
+  unsigned long long* slots = nullptr;
+  ProbeScope(f5h_engine* e_, int kc, hipStream_t s, int* site, DevProbe* kp = nullptr)
+      : e(e_), st(s), on(e_->probe_class == kc && e_->pslots && *site < kProbeSites) {
+    if (!on) return;
+    slots = e->pslots + (size_t)(*site)++ * kProbeRow;
+    if (kp) {
+      self = true;
+      kp->slots = slots;
+      kp->tick = e->ptick;
+    } else {
+      (void)stamp_begin(slots, e->ptick, st);
     }
   }
   ~ProbeScope() {
-    if (!on) return;
-    if (cap)
-      (void)stamp_end(e->pstamp + 64 + idx, e->pstamp, st);
-    else
-      (void)hipEventRecord(e->ev[idx + 1], st);
+    if (on && !self) (void)stamp_end(slots, e->ptick, st);
   }
 };
 
@@ -485,7 +477,7 @@ struct Ctx {
   hipStream_t st;
   Bufs b;
   int B, N, nt, S, L, nfe, use_cfg, batch_mask;
-  int* cap_ev;  // non-null while capturing a step graph (probe stamp-site counter)
+  int site;  // probe launch-site counter, reset at the start of every step's enqueue
 };
 
 static GemmArgs gargs(const void* A, int64_t lda, const Lin& W, int M, void* C, int64_t ldc) {
@@ -615,7 +607,7 @@ static int backbone_step(Ctx& c) {
     cv.mode = 0;
     cv.y = b.c1;
     {
-      ProbeScope ps(e, KC_CONV, st, c.cap_ev);
+      ProbeScope ps(e, KC_CONV, st, &c.site);
       KCK(conv_pos(bf, cv, st));
     }
     cv.x = b.c1;
@@ -664,7 +656,7 @@ static int backbone_step(Ctx& c) {
       g.k = b.k;
       g.v = b.v;
       g.q_scale = 0.125f * 1.4426950408889634f;  // softmax scale 1/sqrt(64) in log2 units, folded into q
-      ProbeScope ps(e, KC_QKV, st, c.cap_ev);
+      ProbeScope ps(e, KC_QKV, st, &c.site, &g.probe);
       KCK(gemm(bf, EPI_QKV, g, st));
     }
     {
@@ -679,18 +671,18 @@ static int backbone_step(Ctx& c) {
       at.kv_len = (a.attn_mask_enabled && c.batch_mask) ? b.kvlen : nullptr;
       at.scale = 0.125f;
       at.prescaled = 1;
-      ProbeScope ps(e, KC_ATTN, st, c.cap_ev);
+      ProbeScope ps(e, KC_ATTN, st, &c.site, &at.probe);
       KCK(attention(bf, at, st));
     }
     {
       GemmArgs g = gargs(b.o, inner, Ly.out, rows, h, d);
       g.gate = ad ? ad + 2 * d : nullptr;  // gate_msa
       g.rowkeep = keep;                    // masked_fill of pad rows (modules.py:552-554)
-      ProbeScope ps(e, KC_OUT, st, c.cap_ev);
+      ProbeScope ps(e, KC_OUT, st, &c.site, &g.probe);
       KCK(gemm(bf, EPI_RESID, g, st));
     }
     {
-      ProbeScope ps(e, KC_NORM, st, c.cap_ev);
+      ProbeScope ps(e, KC_NORM, st, &c.site);
       if (dit)
         KCK(ln_modulate(bf, h, rows, d, ad + 3 * d /*shift_mlp*/, ad + 4 * d /*scale_mlp*/, b.aop, st));
       else
@@ -698,13 +690,13 @@ static int backbone_step(Ctx& c) {
     }
     {
       GemmArgs g = gargs(b.aop, d, Ly.ff1, rows, b.f, a.ff_dim);
-      ProbeScope ps(e, KC_FFN1, st, c.cap_ev);
+      ProbeScope ps(e, KC_FFN1, st, &c.site, &g.probe);
       KCK(gemm(bf, EPI_GELU_TANH, g, st));
     }
     {
       GemmArgs g = gargs(b.f, a.ff_dim, Ly.ff2, rows, h, d);
       g.gate = ad ? ad + 5 * d : nullptr;  // gate_mlp
-      ProbeScope ps(e, KC_FFN2, st, c.cap_ev);
+      ProbeScope ps(e, KC_FFN2, st, &c.site, &g.probe);
       KCK(gemm(bf, EPI_RESID, g, st));
     }
   }
@@ -763,14 +755,15 @@ int f5h_engine_create(const f5h_arch* arch, const f5h_weight* weights, int32_t n
   {
     void* p = nullptr;
     int khz = 0;
-    if (hipMalloc(&p, 4096 * sizeof(unsigned long long)) != hipSuccess ||
-        hipMemset(p, 0, 4096 * sizeof(unsigned long long)) != hipSuccess) {
+    if (hipMalloc(&p, kProbeBytes) != hipSuccess || hipMemset(p, 0, kProbeBytes) != hipSuccess) {
       if (p) (void)hipFree(p);
       f5h_engine_destroy(e);
       return fail(F5H_EHIP, "probe stamp buffer");
     }
     e->allocs.push_back(p);
     e->pstamp = reinterpret_cast<unsigned long long*>(p);
+    e->pslots = e->pstamp + 64;
+    e->ptick = reinterpret_cast<int*>(e->pstamp);
     if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, device) == hipSuccess) e->wall_khz = khz;
   }
   *out = e;
@@ -782,7 +775,6 @@ void f5h_engine_destroy(f5h_engine* e) {
   for (GraphEntry* g : e->graphs) graph_entry_free(g);
   if (e->cap) (void)hipStreamDestroy(e->cap);
   for (void* p : e->allocs) (void)hipFree(p);
-  for (auto x : e->ev) (void)hipEventDestroy(x);
   delete e;
 }
 
@@ -848,6 +840,7 @@ int f5h_sample(f5h_engine* e, void* stream, const f5h_sample_args* a, void* work
 static int enqueue_step(Ctx& c, const f5h_sample_args* a) {
   f5h_engine* e = c.e;
   {
+    c.site = 0;
     RC(step_prep(c));
     RC(backbone_step(c));
     EulerArgs u{};
@@ -869,7 +862,7 @@ static int enqueue_step(Ctx& c, const f5h_sample_args* a) {
     u.traj = nullptr;
     u.trajp = c.b.trajp;
     KCK(cfg_euler(u, c.st));
-    KCK(step_advance(c.b.kstep, c.st));
+    KCK(step_advance(c.b.kstep, e->ptick, c.st));
   }
   return 0;
 }
@@ -889,6 +882,7 @@ static int run_steps(Ctx& c, const f5h_sample_args* a, const void* ws) {
   key.use_cfg = c.use_cfg;
   key.batch_mask = c.batch_mask;
   key.probe = e->probe_class;
+  key.kernel_epoch = g_kernel_epoch.load();
   std::memcpy(&key.cfg_bits, &a->cfg_strength, 4);
   hipGraphExec_t exec = nullptr;
   {
@@ -902,8 +896,6 @@ static int run_steps(Ctx& c, const f5h_sample_args* a, const void* ws) {
       ne->key = key;
       Ctx cc = c;
       cc.st = e->cap;
-      int sites = 0;
-      cc.cap_ev = &sites;
       hipError_t be = hipStreamBeginCapture(e->cap, hipStreamCaptureModeThreadLocal);
       if (be != hipSuccess) {
         graph_entry_free(ne);
@@ -967,8 +959,10 @@ int f5h_forward(f5h_engine* e, void* stream, const f5h_forward_args* a, void* wo
   RC(prologue(c, tg, 1, a->cond, a->cond_mask, a->text, a->duration));
   HIPCK(pack_y(e->bf, a->x, c.B * c.N, e->a.mel_dim, c.b.ypad, c.st));
   HIPCK(hipMemsetAsync(c.b.kstep, 0, sizeof(int), c.st));
+  c.site = 0;
   RC(step_prep(c));
   RC(backbone_step(c));
+  HIPCK(step_advance(c.b.kstep, e->ptick, c.st));
   HIPCK(copy_pred(c.b.p, c.S, c.L, e->a.backbone == F5H_DIT ? 0 : 1, e->a.mel_dim, e->a.mel_dim, a->pred, c.st));
   return 0;
 }
@@ -977,10 +971,14 @@ int f5h_probe_enable(f5h_engine* e, int32_t kclass, int32_t enable) {
   if (!e) return fail(F5H_EINVAL, "null engine");
   std::lock_guard<std::mutex> g(e->pm);
   e->probe_class = enable ? kclass : -1;
-  e->ev_used = 0;
-  e->probe_launches = 0;
-  e->probe_ms = 0.0;
-  if (e->pstamp) HIPCK(hipMemset(e->pstamp, 0, 2 * sizeof(unsigned long long)));
+  if (e->pstamp) {  // tick = 0, start stamps = max, end stamps = 0
+    HIPCK(hipSetDevice(e->dev));
+    HIPCK(hipDeviceSynchronize());
+    HIPCK(hipMemset(e->pstamp, 0, 64 * sizeof(unsigned long long)));
+    HIPCK(hipMemset(e->pslots, 0xff, (size_t)kProbeEnd * sizeof(unsigned long long)));
+    HIPCK(hipMemset(e->pslots + kProbeEnd, 0, (size_t)kProbeEnd * sizeof(unsigned long long)));
+    HIPCK(hipDeviceSynchronize());
+  }
   return 0;
 }
 
@@ -988,21 +986,24 @@ int f5h_probe_read(f5h_engine* e, int64_t* launches, double* total_ms) {
   if (!e) return fail(F5H_EINVAL, "null engine");
   std::lock_guard<std::mutex> g(e->pm);
   double ms = 0.0;
-  for (size_t i = 0; i + 1 < e->ev_used; i += 2) {
-    HIPCK(hipEventSynchronize(e->ev[i + 1]));
-    float t = 0.f;
-    HIPCK(hipEventElapsedTime(&t, e->ev[i], e->ev[i + 1]));
-    ms += t;
-  }
-  int64_t n = (int64_t)(e->ev_used / 2);
-  // step graphs: launches timed by device wall-clock stamps, accumulated on the device
+  int64_t n = 0;
   if (e->pstamp && e->wall_khz > 0.0) {
     HIPCK(hipSetDevice(e->dev));
     HIPCK(hipDeviceSynchronize());
-    unsigned long long acc[2] = {0, 0};
-    HIPCK(hipMemcpy(acc, e->pstamp, sizeof(acc), hipMemcpyDeviceToHost));
-    ms += (double)acc[0] / e->wall_khz;
-    n += (int64_t)acc[1];
+    std::vector<unsigned long long> h(2 * (size_t)kProbeEnd);
+    HIPCK(hipMemcpy(h.data(), e->pslots, h.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+    unsigned long long ticks = 0;
+    for (int64_t i = 0; i < kProbeEnd; i += (int64_t)kProbeLanes * kProbeStride) {  // one (site, tick)
+      unsigned long long t0 = ~0ull, t1 = 0;
+      for (int l = 0; l < kProbeLanes; ++l) {
+        t0 = std::min(t0, h[i + l * kProbeStride]);
+        t1 = std::max(t1, h[kProbeEnd + i + l * kProbeStride]);
+      }
+      if (t1 == 0 || t0 == ~0ull || t1 < t0) continue;  // no finished launch at this site and tick
+      ticks += t1 - t0;
+      ++n;
+    }
+    ms = (double)ticks / e->wall_khz;
   }
   if (launches) *launches = n;
   if (total_ms) *total_ms = ms;
@@ -1062,6 +1063,7 @@ int f5h_op_linear(void* stream, int32_t compute, int32_t M, int32_t N, int32_t K
 int f5h_gemm_force_config(int32_t cfg) {
   if (cfg < -1 || (cfg > 7 && cfg < 10) || cfg > 17) return fail(F5H_EINVAL, "gemm config must be -1..7 or 10..17");
   gemm_force_config(cfg);
+  g_kernel_epoch.fetch_add(1);
   return 0;
 }
 
@@ -1073,6 +1075,7 @@ int f5h_debug_attn_stamps(uint64_t* out, int32_t n) {
 int f5h_attn_force_variant(int32_t v) {
   if (v != -1 && (v < 1 || v > 9)) return fail(F5H_EINVAL, "attention variant must be -1 or 1..9");
   attn_force_variant(v);
+  g_kernel_epoch.fetch_add(1);
   return 0;
 }
 

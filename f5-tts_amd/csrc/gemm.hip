@@ -69,6 +69,14 @@ F5H_DEV V8 load8(const float* p) {
   return V8{{a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w}};
 }
 
+// n / d for 0 <= n < 2^24, d > 0: float quotient + one-step correction (no integer division loop)
+F5H_DEV int fdiv(int n, int d) {
+  int q = (int)((float)n * __builtin_amdgcn_rcpf((float)d));
+  q -= q * d > n;
+  q += (q + 1) * d <= n;
+  return q;
+}
+
 // Apply the epilogue to 8 consecutive columns [col, col+8) of output row `row`.
 template <typename TC, int EPI>
 F5H_DEV void epi8(const GemmArgs& g, int row, int col, V8 x, const V8* pre = nullptr) {
@@ -87,9 +95,9 @@ F5H_DEV void epi8(const GemmArgs& g, int row, int col, V8 x, const V8* pre = nul
     // interleaved RoPE pairs (2i, 2i+1) (x_transformers rotate_half) never straddle an 8-column chunk;
     // a 64-column head maps to one contiguous 128 B row segment of q/k/v [S,H,L,64]
     const int inner = g.heads * 64;
-    const int which = col / inner, hc = col - which * inner;
+    const int which = fdiv(col, inner), hc = col - which * inner;
     const int head = hc >> 6, dh = hc & 63;
-    const int s = row / g.seq_len, pos = row - s * g.seq_len;
+    const int s = fdiv(row, g.seq_len), pos = row - s * g.seq_len;
     if (which < 2 && head < g.rope_heads) {
       const float4* cs = reinterpret_cast<const float4*>(g.rope + (int64_t)pos * 32 + (dh >> 1));
 #pragma unroll
@@ -114,7 +122,7 @@ F5H_DEV void epi8(const GemmArgs& g, int row, int col, V8 x, const V8* pre = nul
   const bool vec = full && (g.ldc % 4 == 0);
   if constexpr (EPI == EPI_GELU_TANH) {
 #pragma unroll
-    for (int e = 0; e < 8; ++e) x.v[e] = gelu_tanh(x.v[e]);
+    for (int e = 0; e < 8; ++e) x.v[e] = std::is_same<TC, bf16>::value ? gelu_tanh_fast(x.v[e]) : gelu_tanh(x.v[e]);
     TC* C = reinterpret_cast<TC*>(g.C);
     if (full && g.ldc % 8 == 0) {
       store8<TC>(C + off, x);
@@ -185,6 +193,7 @@ F5H_DEV void wait_stages(int n_stages) {
 
 template <typename TC, int EPI, int BM, int BN, int WGM, int WGN, int NS>
 __global__ __launch_bounds__(64 * WGM * WGN, 1) void gemm_kernel(GemmArgs g) {
+  const ProbeT probe_t = probe_enter(g.probe);
   typedef GemmCfg<BM, BN, WGM, WGN, NS> C;
   constexpr int E = elems16<TC>();
   constexpr int BKE = 8 * E;
@@ -358,6 +367,7 @@ __global__ __launch_bounds__(64 * WGM * WGN, 1) void gemm_kernel(GemmArgs g) {
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   }
+  probe_exit(g.probe, probe_t);
 }
 
 // ======================================================================================
@@ -407,6 +417,7 @@ struct PPCfg {
 
 template <typename TC, int EPI, int BM, int BN, int WGM2, int WGN2, int KS, int D, int ABL = 0>
 __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(GemmArgs g) {
+  const ProbeT probe_t = probe_enter(g.probe);
   typedef PPCfg<BM, BN, WGM2, WGN2, KS, D> C;
   constexpr int WM = C::WM, WN = C::WN, MT = C::MT, NT = C::NT, NA = C::NA, NB = C::NB;
   constexpr int SB = C::stage_bytes, PB = KS * SB;  // stage / phase bytes
@@ -565,6 +576,7 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(GemmArgs g) {
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   }
+  probe_exit(g.probe, probe_t);
 }
 
 static int gemm_abl() {  // ablation probe (tools): 1 no DMA, 2 no MFMA, 4 no LDS reads in the K loop
@@ -628,6 +640,10 @@ static void launch_cfg(const GemmArgs& a, hipStream_t st) {
 // efficiencies from tools/gemm_tune.py on MI355X (C3-sized GEMMs: 64x128 0.57, 128x128 0.74,
 // 192x128 0.86 of the best). C2 picks 192x128 for QKV, 128x128 for FFN1, 64x128 for N = 1024.
 static int pick_cfg(const GemmArgs& a) {
+  // Large batches (C3/C4/C5: thousands of 256x256 tiles, many rounds per CU): the 8-wave
+  // ping-pong 256x256 kernel (cfg 11), 5-6 % faster than the best 4-wave tile there
+  // (tools/gemm_tune.py: C3 QKV 856 vs 907 us, C3 FFN2 512 vs 544 us).
+  if (a.K % 64 == 0 && (int64_t)((a.M + 255) / 256) * ((a.N + 255) / 256) >= 1024) return 11;
   struct Opt { int cfg, bm, bn; float eff; };
   constexpr Opt opts[3] = {{5, 192, 128, 0.86f}, {1, 128, 128, 0.74f}, {0, 64, 128, 0.57f}};
   int best = 0;

@@ -16,6 +16,19 @@ enum Epi {
   EPI_QKV = 7,        // RoPE + scatter to q/k/v [S,H,L,64]              (operand out)
 };
 
+// In-kernel launch probe (see probe_enter/probe_exit in common.h). Per launch site a row of
+// kProbeTicks x kProbeLanes entries, each on its own 128-B line (kProbeStride words): workgroup b
+// stamps lane b % kProbeLanes, so same-line atomics stay few; the start rows (atomicMin) come
+// first, the end rows (atomicMax) kProbeEnd words further on. Host: min/max over lanes.
+// Only every kProbeEvery-th step tick is stamped (the rest run unperturbed apart from one load).
+constexpr int kProbeTicks = 512, kProbeSites = 64, kProbeLanes = 16, kProbeStride = 16, kProbeEvery = 4;
+constexpr int64_t kProbeRow = (int64_t)kProbeTicks * kProbeLanes * kProbeStride;
+constexpr int64_t kProbeEnd = kProbeRow * kProbeSites;
+struct DevProbe {
+  unsigned long long* slots;  // null: not probed
+  const int* tick;            // device step tick
+};
+
 struct GemmArgs {
   const void* A; int64_t lda;      // [M,K] row-major, TA elements
   const void* W; int64_t ldw;      // [Npad,K] row-major, operand elements (rows padded to 128)
@@ -32,6 +45,7 @@ struct GemmArgs {
   int heads, rope_heads;
   void* q; void* k; void* v;
   float q_scale;                   // EPI_QKV: q is stored pre-multiplied by this (0 -> 1)
+  DevProbe probe;                  // in-kernel launch timing (null slots: off)
 };
 
 // compute: 0 fp32 operands, 1 bf16 operands. A and W both in the operand dtype.
@@ -46,6 +60,7 @@ struct AttnArgs {
   const int32_t* kv_len;  // [S] or null
   float scale;            // 1/sqrt(64)
   int prescaled;          // q already carries scale*log2(e): scores are in log2 units
+  DevProbe probe;         // in-kernel launch timing (null slots: off)
 };
 hipError_t attention(int compute, const AttnArgs& a, hipStream_t st);
 // pin the bf16 attention variant (-1 = default); tuning and test hook
@@ -114,11 +129,11 @@ hipError_t cfg_euler(const EulerArgs& a, hipStream_t st);
 hipError_t grid_upload(const float* t_host, int n, float* out, hipStream_t st);
 // dst[0..n) = src[k*stride ..], k = *kstep (n, stride multiples of 4)
 hipError_t step_begin(const int* kstep, const float* src, int64_t stride, int n, float* dst, hipStream_t st);
-// probe stamps: *slot = wall clock; acc[0] += now - *slot, acc[1] += 1
-hipError_t stamp_begin(unsigned long long* slot, hipStream_t st);
-hipError_t stamp_end(const unsigned long long* slot, unsigned long long* acc, hipStream_t st);
-// *kstep += 1
-hipError_t step_advance(int* kstep, hipStream_t st);
+// probe stamps around a launch (DevProbe slot layout), indexed by *tick
+hipError_t stamp_begin(unsigned long long* slots, const int* tick, hipStream_t st);
+hipError_t stamp_end(unsigned long long* slots, const int* tick, hipStream_t st);
+// *kstep += 1 and *tick += 1 (probe step tick)
+hipError_t step_advance(int* kstep, int* tick, hipStream_t st);
 hipError_t final_where(const float* cond, const uint8_t* cond_mask, float* y, int B, int N, int mel,
                        hipStream_t st);
 hipError_t final_where_out(const float* cond, const uint8_t* cond_mask, const float* y, float* out, int B, int N,
