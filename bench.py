@@ -120,6 +120,7 @@ def main():
     ap.add_argument("--probe", default="attention", help="kernel class timed live (in-kernel device wall-clock stamps) for the roofline")
     ap.add_argument("--config", default="c2", choices=("c2", "c3", "c5"),
                     help="workload (SURVEY §8d); c2 is the headline line")
+    ap.add_argument("--no-vocos", action="store_true", help="skip the +Vocos decode timing (SURVEY §8f1)")
     ap.add_argument("--probe-all", action="store_true",
                     help="after the measurement, time every kernel class in its own loop (table on stderr)")
     args = ap.parse_args()
@@ -216,6 +217,41 @@ def main():
                 print(f"[probe] {kc:9s} sampled launches {n:5d}  avg {avg * 1e3:8.2f} us"
                       + (f"  {fl / (avg * 1e-3) / 1e12:7.1f} TF/s" if fl else ""), file=sys.stderr, flush=True)
 
+    # +Vocos ("report an optional +Vocos RTF once f1 exists"): the reference decodes each
+    # generated mel after sampling (utils_infer.py:506-511, benchmark.py:430-435); timed separately
+    # on the same device, K rounds over this rank's utterances, bf16 backbone + fp32 iSTFT head.
+    vocos = None
+    if not args.no_vocos:
+        from f5_tts_amd.vocos import Vocos, make_weights as vocos_weights
+
+        voc = Vocos(compute="bf16")
+        voc.load_state_dict(vocos_weights())
+        voc.to(device)
+        out, _ = model.sample(cond=cond, text=text, duration=duration, lens=lens, steps=case["nfe"],
+                              cfg_strength=case["cfg"], sway_sampling_coef=case["sway"], seed=rank)
+        gens = [out[b, refs[b]:tots[b]].t().unsqueeze(0).float().contiguous() for b in range(B)]
+        for g in gens:
+            voc.decode(g)
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        tv = time.perf_counter()
+        for _ in range(args.steps):
+            for g in gens:
+                voc.decode(g)
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        vel = time.perf_counter() - tv
+        if world > 1:
+            tt = torch.tensor([vel], device=device, dtype=torch.float64)
+            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+            vel = float(tt.item())
+        v_ms = vel / args.steps * 1e3
+        vocos = {"ms_per_step": round(v_ms, 3), "rtf_with_vocos": round((ms_per_step + v_ms) / 1e3 / (gen_frames * HOP / SR), 5),
+                 "note": "Vocos mel-24khz decode of each generated mel (per utterance, as the reference), "
+                         "synthetic weights; rtf_with_vocos = (CFM + Vocos wall) / generated audio seconds"}
+
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline and args.config == "c2":
         cpu = cpu_baseline(case, arch, threads=min(16, os.cpu_count() or 1))
@@ -249,6 +285,7 @@ def main():
             "rtf": round(rtf, 5),
             "path_tflops": round(flops_call * args.steps * world / elapsed / 1e12, 2),
             "roofline": roof,
+            "vocos": vocos,
             "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)

@@ -33,6 +33,7 @@ static int fail(int code, const std::string& msg) {
   g_err = msg;
   return code;
 }
+int f5h_internal_fail(int code, const std::string& msg) { return fail(code, msg); }
 #define HIPCK(x)                                                                               \
   do {                                                                                         \
     hipError_t _e = (x);                                                                       \

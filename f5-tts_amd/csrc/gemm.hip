@@ -120,9 +120,11 @@ F5H_DEV void epi8(const GemmArgs& g, int row, int col, V8 x, const V8* pre = nul
   }
   const int64_t off = (int64_t)row * g.ldc + col;
   const bool vec = full && (g.ldc % 4 == 0);
-  if constexpr (EPI == EPI_GELU_TANH) {
+  if constexpr (EPI == EPI_GELU_TANH || EPI == EPI_GELU_ERF_OP) {
 #pragma unroll
-    for (int e = 0; e < 8; ++e) x.v[e] = std::is_same<TC, bf16>::value ? gelu_tanh_fast(x.v[e]) : gelu_tanh(x.v[e]);
+    for (int e = 0; e < 8; ++e)
+      x.v[e] = EPI == EPI_GELU_ERF_OP ? gelu_erf(x.v[e])
+                                      : (std::is_same<TC, bf16>::value ? gelu_tanh_fast(x.v[e]) : gelu_tanh(x.v[e]));
     TC* C = reinterpret_cast<TC*>(g.C);
     if (full && g.ldc % 8 == 0) {
       store8<TC>(C + off, x);
@@ -726,6 +728,7 @@ static hipError_t launch_epi(int epi, const GemmArgs& a, hipStream_t st) {
     case EPI_RESID_FILL: return launch_t<TC, EPI_RESID_FILL>(a, st);
     case EPI_INPROJ: return launch_t<TC, EPI_INPROJ>(a, st);
     case EPI_QKV: return launch_t<TC, EPI_QKV>(a, st);
+    case EPI_GELU_ERF_OP: return launch_t<TC, EPI_GELU_ERF_OP>(a, st);
   }
   return hipErrorInvalidValue;
 }

@@ -14,6 +14,7 @@ enum Epi {
   EPI_RESID_FILL = 5, // C = rowkeep[m] ? C + acc + bias : 0             (fp32 in/out)
   EPI_INPROJ = 6,     // C[m] = acc + add[m]; C[m+dual] = acc + add[m+dual]  (fp32)
   EPI_QKV = 7,        // RoPE + scatter to q/k/v [S,H,L,64]              (operand out)
+  EPI_GELU_ERF_OP = 8,  // C = gelu_erf(acc + bias)                      (operand out; Vocos pwconv1)
 };
 
 // In-kernel launch probe (see probe_enter/probe_exit in common.h). Per launch site a row of
@@ -148,6 +149,11 @@ hipError_t build_kvlen(const int32_t* dur, int B, int S, int off, int32_t* kv, h
 hipError_t write_time_token(const float* temb, int S, int L, int d, float* h, hipStream_t st);
 // extract rows [s, 1..L-1] of pred -> dst [S, L-1, mel]
 hipError_t copy_pred(const float* p, int S, int L, int row_off, int mel, int64_t p_ld, float* dst, hipStream_t st);
+// Vocos decoder glue (vocos.hip)
+hipError_t vocos_im2col(int compute, const float* mel, int B, int T, int C, int Kp, void* out, hipStream_t st);
+hipError_t vocos_spec(float* x, int64_t rows, int bins, int ld, hipStream_t st);
+hipError_t vocos_ola(const float* frames, const float* win, int B, int T, int n_fft, int hop, float* y,
+                     hipStream_t st);
 hipError_t f32_to_op(int compute, const float* x, int64_t n, void* out, hipStream_t st);
 hipError_t op_to_f32(int compute, const void* x, int64_t n, float* out, hipStream_t st);
 

@@ -37,6 +37,10 @@ EXPORTS = (
     "f5h_gemm_force_config",
     "f5h_attn_force_variant",
     "f5h_debug_attn_stamps",
+    "f5h_vocos_create",
+    "f5h_vocos_destroy",
+    "f5h_vocos_workspace_size",
+    "f5h_vocos_decode",
     "f5h_last_error",
     "f5h_version",
 )
@@ -48,6 +52,11 @@ class Arch(ctypes.Structure):
     _fields_ = [(n, ctypes.c_int32) for n in (
         "backbone", "dim", "depth", "heads", "dim_head", "ff_dim", "text_dim", "text_num_embeds", "mel_dim",
         "conv_layers", "text_mask_padding", "pe_attn_head", "attn_mask_enabled", "compute")]
+
+
+class VocosArch(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_int32) for n in (
+        "input_channels", "dim", "intermediate_dim", "num_layers", "n_fft", "hop_length", "compute")]
 
 
 class Weight(ctypes.Structure):
@@ -118,6 +127,14 @@ def lib():
     L.f5h_attn_force_variant.restype = ctypes.c_int
     L.f5h_debug_attn_stamps.argtypes = [vp, i32]
     L.f5h_debug_attn_stamps.restype = ctypes.c_int
+    L.f5h_vocos_create.argtypes = [ctypes.POINTER(VocosArch), ctypes.POINTER(Weight), i32, i32, ctypes.POINTER(vp)]
+    L.f5h_vocos_create.restype = ctypes.c_int
+    L.f5h_vocos_destroy.argtypes = [vp]
+    L.f5h_vocos_destroy.restype = None
+    L.f5h_vocos_workspace_size.argtypes = [vp, i32, i32]
+    L.f5h_vocos_workspace_size.restype = sz
+    L.f5h_vocos_decode.argtypes = [vp, vp, i32, i32, vp, vp, vp, sz]
+    L.f5h_vocos_decode.restype = ctypes.c_int
     L.f5h_last_error.argtypes = []
     L.f5h_last_error.restype = ctypes.c_char_p
     L.f5h_version.argtypes = []

@@ -157,6 +157,33 @@ int f5h_attn_force_variant(int32_t variant);
  * pairs x 8 waves x 8 words). */
 int f5h_debug_attn_stamps(uint64_t* out, int32_t n);
 
+/* ---------------------------------------------------------------------------------------
+ * Vocos decoder (mel -> waveform), SURVEY §8(f1): the step after the CFM path, replacing
+ * `vocoder.decode(mel)` (infer/utils_infer.py:510-511; runtime/triton_trtllm/benchmark.py:435)
+ * of the vocos package's mel-24khz model (Vocos.decode = backbone + ISTFTHead). Weights by the
+ * vocos state-dict names ("backbone.embed.weight", "backbone.convnext.{i}.pwconv1.weight",
+ * "head.out.weight", ...), fp32 host arrays. compute: F5H_BF16 runs the backbone GEMMs on bf16
+ * MFMA; the head and the inverse STFT always run in fp32. */
+typedef struct f5h_vocos_arch {
+  int32_t input_channels;    /* 100 mel bins */
+  int32_t dim;               /* 512 */
+  int32_t intermediate_dim;  /* 1536 */
+  int32_t num_layers;        /* 8 */
+  int32_t n_fft;             /* 1024 (win_length = n_fft, hann, center padding) */
+  int32_t hop_length;        /* 256 */
+  int32_t compute;           /* f5h_compute */
+} f5h_vocos_arch;
+typedef struct f5h_vocos f5h_vocos;
+
+int f5h_vocos_create(const f5h_vocos_arch* arch, const f5h_weight* weights, int32_t n_weights, int32_t device,
+                     f5h_vocos** out);
+void f5h_vocos_destroy(f5h_vocos* v);
+size_t f5h_vocos_workspace_size(const f5h_vocos* v, int32_t B, int32_t T);
+/* mel [B][input_channels][T] fp32 (vocos' channel-first layout) -> audio [B][(T-1)*hop] fp32
+ * (torch.istft center=True length). Device pointers; work enqueued on `stream`. */
+int f5h_vocos_decode(f5h_vocos* v, void* stream, int32_t B, int32_t T, const float* mel, float* audio,
+                     void* workspace, size_t workspace_bytes);
+
 const char* f5h_last_error(void);
 const char* f5h_version(void);
 

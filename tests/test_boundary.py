@@ -57,6 +57,7 @@ int main(void) {{
   printf("%zu %zu %zu %zu\\n", sizeof(f5h_arch), sizeof(f5h_weight), sizeof(f5h_sample_args), sizeof(f5h_forward_args));
   printf("%zu %zu %zu %zu\\n", offsetof(f5h_sample_args, cfg_strength), offsetof(f5h_sample_args, out),
          offsetof(f5h_forward_args, t), offsetof(f5h_forward_args, pred));
+  printf("%zu %zu\\n", sizeof(f5h_vocos_arch), offsetof(f5h_vocos_arch, compute));
   return 0;
 }}""")
     exe = tmp_path / "layout"
@@ -64,7 +65,8 @@ int main(void) {{
     got = subprocess.run([str(exe)], capture_output=True, text=True, check=True).stdout.split()
     want = [ctypes.sizeof(_lib.Arch), ctypes.sizeof(_lib.Weight), ctypes.sizeof(_lib.SampleArgs),
             ctypes.sizeof(_lib.ForwardArgs), _lib.SampleArgs.cfg_strength.offset, _lib.SampleArgs.out.offset,
-            _lib.ForwardArgs.t.offset, _lib.ForwardArgs.pred.offset]
+            _lib.ForwardArgs.t.offset, _lib.ForwardArgs.pred.offset,
+            ctypes.sizeof(_lib.VocosArch), _lib.VocosArch.compute.offset]
     assert [int(x) for x in got] == want
 
 
@@ -79,6 +81,9 @@ def test_errors_are_reported_not_crashing():
     h = ctypes.c_void_p()
     rc = L.f5h_engine_create(ctypes.byref(a), None, 0, 0, ctypes.byref(h))
     assert rc == -1 and b"multiple of 128" in L.f5h_last_error()
+    va = _lib.VocosArch(100, 500, 1536, 8, 1024, 256, 0)
+    rc = L.f5h_vocos_create(ctypes.byref(va), None, 0, 0, ctypes.byref(h))
+    assert rc == -1 and b"bad vocos arch" in L.f5h_last_error()
 
 
 def test_no_cpu_fallback_in_product_path():
