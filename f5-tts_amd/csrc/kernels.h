@@ -154,6 +154,10 @@ hipError_t vocos_im2col(int compute, const float* mel, int B, int T, int C, int 
 hipError_t vocos_spec(float* x, int64_t rows, int bins, int ld, hipStream_t st);
 hipError_t vocos_ola(const float* frames, const float* win, int B, int T, int n_fft, int hop, float* y,
                      hipStream_t st);
+// log-mel front end glue (melspec.hip)
+hipError_t mel_frames(const float* wav, int B, int L, int T, int n_fft, int hop, float* frames, hipStream_t st);
+hipError_t mel_mag(const float* spec, int64_t rows, int bins, int ld_spec, int ld_mag, float* mag, hipStream_t st);
+hipError_t mel_log(const float* mel, int B, int T, int n_mels, float* out, hipStream_t st);
 hipError_t f32_to_op(int compute, const float* x, int64_t n, void* out, hipStream_t st);
 hipError_t op_to_f32(int compute, const void* x, int64_t n, float* out, hipStream_t st);
 

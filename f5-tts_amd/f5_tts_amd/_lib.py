@@ -41,6 +41,10 @@ EXPORTS = (
     "f5h_vocos_destroy",
     "f5h_vocos_workspace_size",
     "f5h_vocos_decode",
+    "f5h_mel_create",
+    "f5h_mel_destroy",
+    "f5h_mel_workspace_size",
+    "f5h_mel_forward",
     "f5h_last_error",
     "f5h_version",
 )
@@ -57,6 +61,10 @@ class Arch(ctypes.Structure):
 class VocosArch(ctypes.Structure):
     _fields_ = [(n, ctypes.c_int32) for n in (
         "input_channels", "dim", "intermediate_dim", "num_layers", "n_fft", "hop_length", "compute")]
+
+
+class MelArch(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_int32) for n in ("n_fft", "hop_length", "n_mels", "sample_rate")]
 
 
 class Weight(ctypes.Structure):
@@ -135,6 +143,14 @@ def lib():
     L.f5h_vocos_workspace_size.restype = sz
     L.f5h_vocos_decode.argtypes = [vp, vp, i32, i32, vp, vp, vp, sz]
     L.f5h_vocos_decode.restype = ctypes.c_int
+    L.f5h_mel_create.argtypes = [ctypes.POINTER(MelArch), i32, ctypes.POINTER(vp)]
+    L.f5h_mel_create.restype = ctypes.c_int
+    L.f5h_mel_destroy.argtypes = [vp]
+    L.f5h_mel_destroy.restype = None
+    L.f5h_mel_workspace_size.argtypes = [vp, i32, i32]
+    L.f5h_mel_workspace_size.restype = sz
+    L.f5h_mel_forward.argtypes = [vp, vp, i32, i32, vp, vp, vp, sz]
+    L.f5h_mel_forward.restype = ctypes.c_int
     L.f5h_last_error.argtypes = []
     L.f5h_last_error.restype = ctypes.c_char_p
     L.f5h_version.argtypes = []

@@ -1,36 +1,21 @@
-"""Vocos-style log-mel front end (reference `model/modules.py:80-151`).
+"""Vocos log-mel front end on the HIP engine (reference `model/modules.py:80-151`).
 
-The reference builds `torchaudio.transforms.MelSpectrogram(sample_rate=24000, n_fft=1024,
-win_length=1024, hop_length=256, n_mels=100, power=1, center=True, normalized=False,
-norm=None)` and returns `log(clamp(mel, 1e-5))`. torchaudio is not installed in this image,
-so the transform is restated: periodic Hann window, reflect-padded centred STFT, magnitude
-(power 1), HTK-scale triangular filterbank (torchaudio.functional.melscale_fbanks with
-norm=None, mel_scale="htk", f_min=0, f_max=sr/2). Parity of this row is "unpinned": no
-reference fixture exists in-tree and torchaudio cannot be imported here.
-
-This runs before the sampling engine (cfm.py:106-108) and is host/torch code, not part of
-the HIP hot path.
+`MelSpec` keeps the reference module's constructor and call surface (wav [B, L] or [B, 1, L] ->
+log-mel [B, n_mels, 1 + L // hop]) and runs `f5h_mel_forward` (include/f5h.h): reflect-padded
+frames, DFT and HTK filterbank as fp32 MFMA GEMMs, magnitude and clamp/log kernels. CFM.sample
+calls it on raw-audio conditioning (cfm.py:106-108). There is no PyTorch fallback; the CPU
+restatement used to check it lives in oracle/mel_cpu.py.
 """
 
 from __future__ import annotations
 
-import math
+import ctypes
+import threading
 
 import torch
 from torch import nn
 
-
-def melscale_fbanks(n_freqs: int, f_min: float, f_max: float, n_mels: int, sample_rate: int) -> torch.Tensor:
-    all_freqs = torch.linspace(0, sample_rate // 2, n_freqs)
-    m_min = 2595.0 * math.log10(1.0 + f_min / 700.0)
-    m_max = 2595.0 * math.log10(1.0 + f_max / 700.0)
-    m_pts = torch.linspace(m_min, m_max, n_mels + 2)
-    f_pts = 700.0 * (10 ** (m_pts / 2595.0) - 1.0)
-    f_diff = f_pts[1:] - f_pts[:-1]
-    slopes = f_pts.unsqueeze(0) - all_freqs.unsqueeze(1)
-    down = (-1.0 * slopes[:, :-2]) / f_diff[:-1]
-    up = slopes[:, 2:] / f_diff[1:]
-    return torch.max(torch.zeros(1), torch.min(down, up))  # [n_freqs, n_mels]
+from . import _lib
 
 
 class MelSpec(nn.Module):
@@ -38,20 +23,47 @@ class MelSpec(nn.Module):
                  mel_spec_type="vocos"):
         super().__init__()
         if mel_spec_type != "vocos":
-            raise NotImplementedError("only the vocos mel front end is restated (bigvgan's vocoder is not shipped)")
+            raise NotImplementedError("only the vocos mel front end is provided (bigvgan's vocoder is not shipped)")
+        if win_length != n_fft:
+            raise NotImplementedError("win_length must equal n_fft (the vocos front end)")
         self.n_fft, self.hop_length, self.win_length = n_fft, hop_length, win_length
         self.n_mel_channels, self.target_sample_rate = n_mel_channels, target_sample_rate
-        self.register_buffer("window", torch.hann_window(win_length), persistent=False)
-        self.register_buffer("fb", melscale_fbanks(n_fft // 2 + 1, 0.0, float(target_sample_rate // 2),
-                                                   n_mel_channels, target_sample_rate), persistent=False)
+        self._h = {}
+        self._lock = threading.Lock()
+
+    def _engine(self, device: torch.device):
+        h = self._h.get(device.index)
+        if h is None:
+            a = _lib.MelArch(self.n_fft, self.hop_length, self.n_mel_channels, self.target_sample_rate)
+            h = ctypes.c_void_p()
+            with torch.cuda.device(device):
+                _lib.check(_lib.lib().f5h_mel_create(ctypes.byref(a), device.index, ctypes.byref(h)), "f5h_mel_create")
+            self._h[device.index] = h
+        return h
 
     def forward(self, wav: torch.Tensor) -> torch.Tensor:
         if wav.ndim == 3:
             wav = wav.squeeze(1)
         assert wav.ndim == 2
-        win = self.window.to(wav.device, wav.dtype)
-        spec = torch.stft(wav, self.n_fft, hop_length=self.hop_length, win_length=self.win_length, window=win,
-                          center=True, pad_mode="reflect", normalized=False, onesided=True, return_complex=True)
-        spec = spec.abs()  # power = 1
-        mel = torch.matmul(spec.transpose(-1, -2), self.fb.to(spec.device, spec.dtype)).transpose(-1, -2)
-        return mel.clamp(min=1e-5).log()  # [b, n_mels, frames]
+        if wav.device.type != "cuda":
+            raise RuntimeError("MelSpec runs on the HIP engine: move the waveform to a GPU device")
+        dev = torch.device("cuda", wav.device.index if wav.device.index is not None else torch.cuda.current_device())
+        B, L = wav.shape
+        wav = wav.to(torch.float32).contiguous()
+        T = 1 + L // self.hop_length
+        out = torch.empty(B, self.n_mel_channels, T, dtype=torch.float32, device=dev)
+        with self._lock:
+            h = self._engine(dev)
+            L_ = _lib.lib()
+            ws = torch.empty(max(int(L_.f5h_mel_workspace_size(h, B, L)), 256), dtype=torch.uint8, device=dev)
+            with torch.cuda.device(dev):
+                _lib.check(L_.f5h_mel_forward(h, _lib.stream_handle(dev), B, L, wav.data_ptr(), out.data_ptr(),
+                                              ws.data_ptr(), ws.numel()), "f5h_mel_forward")
+        return out
+
+    def __del__(self):
+        for h in getattr(self, "_h", {}).values():
+            try:
+                _lib.lib().f5h_mel_destroy(h)
+            except Exception:
+                pass

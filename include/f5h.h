@@ -184,6 +184,27 @@ size_t f5h_vocos_workspace_size(const f5h_vocos* v, int32_t B, int32_t T);
 int f5h_vocos_decode(f5h_vocos* v, void* stream, int32_t B, int32_t T, const float* mel, float* audio,
                      void* workspace, size_t workspace_bytes);
 
+/* ---------------------------------------------------------------------------------------
+ * Log-mel front end (wav -> mel), SURVEY §8(f2): replaces get_vocos_mel_spectrogram
+ * (model/modules.py:80-109; torchaudio MelSpectrogram power 1, center/reflect, periodic Hann,
+ * htk filterbank without norm, f_max = sr/2; then clamp(1e-5).log()), which CFM.sample applies
+ * to raw-audio conditioning (cfm.py:106-108). fp32 throughout (DFT and filterbank on fp32 MFMA). */
+typedef struct f5h_mel_arch {
+  int32_t n_fft;        /* 1024 (= win_length) */
+  int32_t hop_length;   /* 256 */
+  int32_t n_mels;       /* 100 */
+  int32_t sample_rate;  /* 24000 */
+} f5h_mel_arch;
+typedef struct f5h_mel f5h_mel;
+
+int f5h_mel_create(const f5h_mel_arch* arch, int32_t device, f5h_mel** out);
+void f5h_mel_destroy(f5h_mel* m);
+/* frames T = 1 + L / hop (torch.stft center=True); L must exceed n_fft/2 (reflect padding) */
+size_t f5h_mel_workspace_size(const f5h_mel* m, int32_t B, int32_t L);
+/* wav [B][L] fp32 -> mel [B][n_mels][T] fp32 (device pointers, enqueued on `stream`) */
+int f5h_mel_forward(f5h_mel* m, void* stream, int32_t B, int32_t L, const float* wav, float* mel, void* workspace,
+                    size_t workspace_bytes);
+
 const char* f5h_last_error(void);
 const char* f5h_version(void);
 
