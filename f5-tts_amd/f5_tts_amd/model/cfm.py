@@ -61,7 +61,8 @@ class CFM(nn.Module):
                keep_trajectory: bool = True):
         """Same arguments/returns as the reference `CFM.sample`; extra keyword `y0` supplies the
         initial noise explicitly (parity tests), `keep_trajectory=False` skips the [steps+1,...] copy."""
-        self.eval()
+        if self.training:
+            self.eval()
         if duplicate_test:
             raise NotImplementedError("duplicate_test is a debugging corner of the reference (cfm.py:141-143)")
         pdtype = next(self.parameters()).dtype
@@ -81,14 +82,18 @@ class CFM(nn.Module):
                 text = list_str_to_tensor(text).to(device)
             assert text.shape[0] == batch
 
-        cond_mask = lens_to_mask(lens)
-        if edit_mask is not None:
-            cond_mask = cond_mask & edit_mask
         if isinstance(duration, int):
             duration = torch.full((batch,), duration, device=device, dtype=torch.long)
         duration = torch.maximum(torch.maximum((text != -1).sum(dim=-1), lens) + 1, duration)
         duration = duration.clamp(max=max_duration)
-        max_duration = int(duration.amax())
+        # the one host sync of the preamble: every per-utterance length at once (the shapes below and
+        # the noise recipe need them on the host)
+        dur_host = [int(d) for d in duration.tolist()]
+        max_duration = max(dur_host)
+        if edit_mask is not None:
+            cond_mask = lens_to_mask(lens) & edit_mask
+        else:  # == F.pad(lens_to_mask(lens), ...) below: max_duration > lens.amax() by the rule above
+            cond_mask = lens_to_mask(lens, length=max_duration)
 
         cond = F.pad(cond, (0, 0, 0, max_duration - cond_seq_len), value=0.0)
         if no_ref_audio:
@@ -98,14 +103,15 @@ class CFM(nn.Module):
 
         if y0 is None:  # noise recipe of cfm.py:196-201 (per utterance, same seed each)
             ys = []
-            for dur in duration:
+            for dur in dur_host:
                 if exists(seed):
                     torch.manual_seed(seed)
-                ys.append(torch.randn(int(dur), self.num_channels, device=self.device, dtype=pdtype))
+                ys.append(torch.randn(dur, self.num_channels, device=self.device, dtype=pdtype))
             y0 = pad_sequence(ys, padding_value=0, batch_first=True)
 
-        t = time_grid(steps, sway_sampling_coef, use_epss, device=self.device, dtype=pdtype)
-        t_host = t.float().cpu().numpy()
+        # the grid is a host constant of the call: built on the CPU in the parameter dtype (cfm.py:211-216)
+        t = time_grid(steps, sway_sampling_coef, use_epss, device="cpu", dtype=pdtype)
+        t_host = t.float().numpy()
 
         eng = self.transformer.get_engine(self.engine_compute(), self.device)
         out, traj = eng.sample(cond.float(), cond_mask, text, duration, y0.float(), t_host, float(cfg_strength),
