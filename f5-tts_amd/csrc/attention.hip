@@ -313,7 +313,10 @@ __global__ __launch_bounds__(256, 2) void attn_bf16_kernel(AttnArgs a) {
 //     adds), summed from the same bf16 P that enters O.
 //   * NW waves x 32 query rows per workgroup (NW = 8: 256 rows, one workgroup per CU at C2),
 //     K/V tiles of 64 keys by LDS-DMA into a 3-deep ring shared by all waves.
-template <bool PRESCALED, int NW>
+// PRIO (wave priority experiments, cdna_hip_programming.md T5): 0 none; 1 = s_setprio 1 once for
+// the second half of the waves (they win VALU/MFMA arbitration, which breaks the two waves of a
+// SIMD out of lockstep); 2 = s_setprio 1 around every MFMA cluster.
+template <bool PRESCALED, int NW, int PRIO = 0>
 __global__ __launch_bounds__(64 * NW, 1) void attn_bf16_v2_kernel(AttnArgs a) {
   const ProbeT probe_t = probe_enter(a.probe);
   constexpr int TILE_B = 2 * 64 * 128;  // K + V tile bytes (64 keys x 64 dh bf16 each)
@@ -391,7 +394,11 @@ __global__ __launch_bounds__(64 * NW, 1) void attn_bf16_v2_kernel(AttnArgs a) {
   const bf16 one = f2bf(1.f);
   const bf16x8 ones = {one, one, one, one, one, one, one, one};
   float m_run = 0.f;  // running max (log2 units), valid after tile 0
-  f32x16 oacc[2], lacc;
+  f32x16 oacc[2], lacc, negm;  // negm (PRIO 3): -m_run broadcast as the QK chains' first C operand
+  if constexpr (PRIO == 3) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) negm[r] = 0.f;
+  }
 #pragma unroll
   for (int r = 0; r < 16; ++r) {
     oacc[0][r] = 0.f;
@@ -401,6 +408,9 @@ __global__ __launch_bounds__(64 * NW, 1) void attn_bf16_v2_kernel(AttnArgs a) {
 
   dma(0, 0);
   if (ntile > 1) dma(1, 1);
+  if constexpr (PRIO == 1) {
+    if (wid >= NW / 2) __builtin_amdgcn_s_setprio(1);
+  }
   for (int kt = 0; kt < ntile; ++kt) {
     if (kt + 1 < ntile)
       asm volatile("s_waitcnt vmcnt(%0)" ::"i"(2 * CPW) : "memory");
@@ -438,15 +448,28 @@ __global__ __launch_bounds__(64 * NW, 1) void attn_bf16_v2_kernel(AttnArgs a) {
     // ---- S^T - m_run = K Q^T + (-m_run)
     const float init = kt == 0 ? 0.f : -m_run;
     f32x16 sacc[2];
+    if constexpr (PRIO == 2) __builtin_amdgcn_s_setprio(1);
+    if constexpr (PRIO == 3) {  // chains start from negm (kept equal to -m_run; 0 before tile 0)
 #pragma unroll
-    for (int t = 0; t < 2; ++t) {
+      for (int t = 0; t < 2; ++t) {
+        sacc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, kf[t][0]), qf[0], negm, 0, 0, 0);
 #pragma unroll
-      for (int r = 0; r < 16; ++r) sacc[t][r] = init;
+        for (int ks = 1; ks < 4; ++ks)
+          sacc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, kf[t][ks]), qf[ks], sacc[t],
+                                                             0, 0, 0);
+      }
+    } else {
 #pragma unroll
-      for (int ks = 0; ks < 4; ++ks)
-        sacc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, kf[t][ks]), qf[ks], sacc[t],
-                                                           0, 0, 0);
+      for (int t = 0; t < 2; ++t) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) sacc[t][r] = init;
+#pragma unroll
+        for (int ks = 0; ks < 4; ++ks)
+          sacc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, kf[t][ks]), qf[ks], sacc[t],
+                                                             0, 0, 0);
+      }
     }
+    if constexpr (PRIO == 2) __builtin_amdgcn_s_setprio(0);
     vread(std::integral_constant<int, 0>{});
     if (kt * 64 + 64 > klen) {  // ragged last tile: keys past klen get p = 0
       const int kbase = kt * 64 + 4 * h;
@@ -457,14 +480,30 @@ __global__ __launch_bounds__(64 * NW, 1) void attn_bf16_v2_kernel(AttnArgs a) {
           if (kbase + t * 32 + (r & 3) + 8 * (r >> 2) >= klen) sacc[t][r] = -INFINITY;
     }
     float mx = -INFINITY;
+    if constexpr (PRIO == 3) {  // 16 v_max3 in two chains (fmaxf would add canonicalising v_max x,x)
+      float mb = -INFINITY;
 #pragma unroll
-    for (int t = 0; t < 2; ++t)
+      for (int t = 0; t < 2; ++t)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) mx = fmaxf(mx, sacc[t][r]);
+        for (int r = 0; r < 16; r += 4) {
+          asm("v_max3_f32 %0, %1, %2, %3" : "=v"(mx) : "v"(mx), "v"(sacc[t][r]), "v"(sacc[t][r + 1]));
+          asm("v_max3_f32 %0, %1, %2, %3" : "=v"(mb) : "v"(mb), "v"(sacc[t][r + 2]), "v"(sacc[t][r + 3]));
+        }
+      mx = fmaxf(mx, mb);
+    } else {
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) mx = fmaxf(mx, sacc[t][r]);
+    }
     mx = fmaxf(mx, xor32(mx));
     if (kt == 0) {
       // first tile (>= 1 valid key): the running max starts at the tile max
       m_run = mx;
+      if constexpr (PRIO == 3) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) negm[r] = -m_run;
+      }
 #pragma unroll
       for (int t = 0; t < 2; ++t)
 #pragma unroll
@@ -474,6 +513,10 @@ __global__ __launch_bounds__(64 * NW, 1) void attn_bf16_v2_kernel(AttnArgs a) {
       const float d = fmaxf(mx, 0.f);
       const float alpha = __builtin_amdgcn_exp2f(-d);
       m_run += d;
+      if constexpr (PRIO == 3) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) negm[r] = -m_run;
+      }
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         oacc[0][r] *= alpha;
@@ -510,6 +553,7 @@ __global__ __launch_bounds__(64 * NW, 1) void attn_bf16_v2_kernel(AttnArgs a) {
           asm volatile("" : "+v"(vf[u][t][sx][1]));
         }
       __builtin_amdgcn_sched_barrier(0);
+      if constexpr (PRIO == 2) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
       for (int t = 0; t < 2; ++t)
 #pragma unroll
@@ -518,6 +562,7 @@ __global__ __launch_bounds__(64 * NW, 1) void attn_bf16_v2_kernel(AttnArgs a) {
           oacc[u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, w), pf[t][sx], oacc[u], 0, 0,
                                                             0);
         }
+      if constexpr (PRIO == 2) __builtin_amdgcn_s_setprio(0);
       __builtin_amdgcn_sched_barrier(0);
     };
     asm volatile("s_waitcnt lgkmcnt(8)" ::: "memory");
@@ -525,6 +570,683 @@ __global__ __launch_bounds__(64 * NW, 1) void attn_bf16_v2_kernel(AttnArgs a) {
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     pv(std::integral_constant<int, 1>{});
   }
+  const float l_tot = lacc[0];
+  const float inv = l_tot > 0.f ? 1.f / l_tot : 0.f;
+  if (qrow < L) {
+    bf16* O = reinterpret_cast<bf16*>(a.o) + (((int64_t)s_idx * L + qrow) * a.H + head) * 64;
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+      for (int r4 = 0; r4 < 4; ++r4) {
+        bf16x4 w = {f2bf(oacc[u][4 * r4 + 0] * inv), f2bf(oacc[u][4 * r4 + 1] * inv),
+                    f2bf(oacc[u][4 * r4 + 2] * inv), f2bf(oacc[u][4 * r4 + 3] * inv)};
+        *reinterpret_cast<bf16x4*>(O + 32 * u + 8 * r4 + 4 * h) = w;
+      }
+  }
+  probe_exit(a.probe, probe_t);
+}
+
+// ---------------------------------------------------------------- bf16 kernel, v8 (software-pipelined)
+// v2's arithmetic with the softmax of tile j-1 moved under the MFMAs of tile j inside each wave
+// (cdna_hip_programming.md T15; an MFMA holds the SIMD's vector issue for 8 of its 32 cycles,
+// MI355X_MICROARCH.md cycle constants), so the two waves of a SIMD need not take turns:
+//   phase A(j): S_j^T - m = K_j Q^T - m (8 MFMA)   ||  P_{j-1} = bf16(exp2(S_{j-1} - m)) (32 exp + 16 pack)
+//   phase B(j): l += 1 P_{j-1}, O += V_{j-1} P_{j-1} (12 MFMA)  ||  row max of S_j
+//   then the lazy re-base of tile j (rare) and the swap of the two S buffers.
+// K/V tiles of 64 keys ride a 4-slot LDS-DMA ring, two tiles ahead: the V of tile j-1 is read
+// in iteration j, so its slot is refilled only at iteration j+1 (with tile j+3).
+template <bool PRESCALED, int NW>
+__global__ __launch_bounds__(64 * NW, 1) void attn_bf16_v8_kernel(AttnArgs a) {
+  const ProbeT probe_t = probe_enter(a.probe);
+  constexpr int TILE_B = 2 * 64 * 128;  // K + V tile bytes (64 keys x 64 dh bf16 each)
+  constexpr int NS = 4;
+  constexpr int CPW = 512 / (64 * NW);  // 16-B chunks of one K (or V) tile per lane
+  constexpr float THR = 8.f;
+  static_assert(CPW * 64 * NW == 512, "whole DMA rounds");
+  __shared__ __attribute__((aligned(16))) uint4 lds[NS * TILE_B / 16];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int h = lane >> 5;
+  int qb, bh;
+  attn_block(qb, bh);
+  const int s_idx = bh / a.H, head = bh - s_idx * a.H;
+  const int L = a.L;
+  const int64_t base = (int64_t)bh * L * 64;
+  const bf16* Q = reinterpret_cast<const bf16*>(a.q) + base;
+  const bf16* K = reinterpret_cast<const bf16*>(a.k) + base;
+  const bf16* V = reinterpret_cast<const bf16*>(a.v) + base;
+  int klen = L;
+  if (a.kv_len) klen = min(klen, a.kv_len[s_idx]);
+  const int ntile = (klen + 63) / 64;
+
+  const int qrow = qb * (32 * NW) + wid * 32 + (lane & 31);
+  bf16x8 qf[4];
+#pragma unroll
+  for (int ks = 0; ks < 4; ++ks) {
+    uint4 v = *reinterpret_cast<const uint4*>(Q + (int64_t)min(qrow, L - 1) * 64 + ks * 16 + h * 8);
+    qf[ks] = __builtin_bit_cast(bf16x8, v);
+    if constexpr (!PRESCALED) {
+      const float c = a.scale * 1.4426950408889634f;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) qf[ks][j] = f2bf(bf2f(qf[ks][j]) * c);
+    }
+  }
+#pragma unroll
+  for (int ks = 0; ks < 4; ++ks) asm volatile("" ::"v"(qf[ks]));
+
+  int dsrc[CPW];
+#pragma unroll
+  for (int r = 0; r < CPW; ++r) {
+    const int p = (r * NW + wid) * 64 + lane, row = p >> 3, slot = p & 7;
+    dsrc[r] = swz128(row, slot) * 8;
+  }
+  auto dma = [&](int kt) {
+    uint4* Ks = lds + (kt % NS) * (TILE_B / 16);
+    uint4* Vs = Ks + 512;
+#pragma unroll
+    for (int r = 0; r < CPW; ++r) {
+      const int row = ((r * NW + wid) * 64 + lane) >> 3;
+      const int64_t off = (int64_t)min(kt * 64 + row, L - 1) * 64 + dsrc[r];
+      __builtin_amdgcn_global_load_lds((const void*)(K + off), (LDS_PTR(void))(Ks + (r * NW + wid) * 64), 16, 0, 0);
+      __builtin_amdgcn_global_load_lds((const void*)(V + off), (LDS_PTR(void))(Vs + (r * NW + wid) * 64), 16, 0, 0);
+    }
+  };
+
+  const uint32_t lds0 = (uint32_t)(uintptr_t)(LDS_PTR(void))lds;
+  uint32_t kaddr[4];
+#pragma unroll
+  for (int ks = 0; ks < 4; ++ks) {
+    const int row = lane & 31;
+    kaddr[ks] = lds0 + row * 128 + swz128(row, ks * 2 + h) * 16;
+  }
+  const int G = lane >> 4, q4 = (lane & 15) >> 2, p4 = lane & 3;
+  uint32_t vaddr[2][2];
+#pragma unroll
+  for (int u = 0; u < 2; ++u)
+#pragma unroll
+    for (int g8 = 0; g8 < 2; ++g8) {
+      const int r1 = 4 * (G >> 1) + q4 + 8 * g8;
+      const int dh = 32 * u + 16 * (G & 1) + 4 * p4;
+      vaddr[u][g8] = lds0 + 64 * 128 + r1 * 128 + swz128(r1, dh >> 3) * 16 + ((dh >> 2) & 1) * 8;
+    }
+
+  const bf16 one = f2bf(1.f);
+  const bf16x8 ones = {one, one, one, one, one, one, one, one};
+  float m_run = 0.f;
+  f32x16 oacc[2], lacc, sA[2], sB[2], negm;  // negm: -m_run broadcast, the QK chains' first C operand
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    oacc[0][r] = 0.f;
+    oacc[1][r] = 0.f;
+    lacc[r] = 0.f;
+  }
+
+  // K fragments of tile kt (issued and retired here; only LDS op in flight at this point)
+  auto kread = [&](int kt, u32x4 (&kf)[2][4]) {
+    const uint32_t so = (uint32_t)((kt % NS) * TILE_B);
+    static_for<0, 4>([&](auto KS) {
+      constexpr int ks = decltype(KS)::value;
+      kf[0][ks] = lds_b128<0>(kaddr[ks] + so);
+      kf[1][ks] = lds_b128<4096>(kaddr[ks] + so);
+    });
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) asm volatile("" : "+v"(kf[t][ks]));
+  };
+  // V^T fragments of tile kt (retired by the caller's lgkmcnt(0) before the PV MFMAs)
+  auto vread = [&](int kt, uint2 (&vf)[2][2][2][2]) {
+    const uint32_t so = (uint32_t)((kt % NS) * TILE_B);
+    static_for<0, 2>([&](auto U) {
+      constexpr int u = decltype(U)::value;
+      static_for<0, 2>([&](auto T) {
+        constexpr int t = decltype(T)::value;
+        static_for<0, 2>([&](auto S) {
+          constexpr int sx = decltype(S)::value;
+          vf[u][t][sx][0] = lds_tr_b64<(32 * t + 16 * sx) * 128>(vaddr[u][0] + so);
+          vf[u][t][sx][1] = lds_tr_b64<(32 * t + 16 * sx) * 128>(vaddr[u][1] + so);
+        });
+      });
+    });
+  };
+  auto mask_tail = [&](int kt, f32x16 (&sc)[2]) {
+    if (kt * 64 + 64 > klen) {  // ragged last tile: keys past klen get p = 0
+      const int kbase = kt * 64 + 4 * h;
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+          if (kbase + t * 32 + (r & 3) + 8 * (r >> 2) >= klen) sc[t][r] = -INFINITY;
+    }
+  };
+  auto rowmax = [&](const f32x16 (&sc)[2]) {
+    float mx = -INFINITY;
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) mx = fmaxf(mx, sc[t][r]);
+    return fmaxf(mx, xor32(mx));
+  };
+  // PV of the previous tile: l += 1 P^T, O += V^T P^T
+  auto pv = [&](const bf16x8 (&pf)[2][2], uint2 (&vf)[2][2][2][2]) {
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int sx = 0; sx < 2; ++sx) lacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ones, pf[t][sx], lacc, 0, 0, 0);
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int sx = 0; sx < 2; ++sx) {
+          const uint4 w = make_uint4(vf[u][t][sx][0].x, vf[u][t][sx][0].y, vf[u][t][sx][1].x, vf[u][t][sx][1].y);
+          oacc[u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, w), pf[t][sx], oacc[u], 0, 0, 0);
+        }
+  };
+
+  // ---- tile 0: S_0, m_run = its row max (exact first-tile base)
+  dma(0);
+  if (ntile > 1) dma(1);
+  {
+    if (ntile > 1)
+      asm volatile("s_waitcnt vmcnt(%0)" ::"i"(2 * CPW) : "memory");
+    else
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    if (ntile > 2) dma(2);
+    u32x4 kf[2][4];
+    kread(0, kf);
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) sA[t][r] = 0.f;
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks)
+        sA[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, kf[t][ks]), qf[ks], sA[t], 0, 0, 0);
+    }
+    mask_tail(0, sA);
+    m_run = rowmax(sA);
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) sA[t][r] -= m_run;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) negm[r] = -m_run;
+  }
+
+  // ---- iteration kt >= 1: S_kt into `cur`, softmax + PV of tile kt-1 from `prev`
+  auto step = [&](int kt, f32x16 (&cur)[2], f32x16 (&prev)[2]) {
+    if (kt + 1 < ntile)
+      asm volatile("s_waitcnt vmcnt(%0)" ::"i"(2 * CPW) : "memory");
+    else
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    if (kt + 2 < ntile) dma(kt + 2);
+    u32x4 kf[2][4];
+    kread(kt, kf);
+    uint2 vf[2][2][2][2];
+    vread(kt - 1, vf);
+    __builtin_amdgcn_sched_barrier(0);
+    // phase A: QK^T of tile kt || exp/pack of tile kt-1, hand-interleaved (sched_barrier fences):
+    // MFMA (t, ks) alternates the two accumulator chains; each gap carries 4 exp2 + 2 packs.
+    bf16x8 pf[2][2];
+    __builtin_amdgcn_sched_barrier(0);
+    static_for<0, 8>([&](auto I) {
+      constexpr int i = decltype(I)::value;
+      constexpr int t = i & 1, ks = i >> 1;           // MFMA chain t, k-step ks
+      constexpr int et = i >> 2, esx = (i >> 1) & 1, ej = (i & 1) * 4;  // exp chunk of tile kt-1
+      cur[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, kf[t][ks]), qf[ks],
+                                                        ks == 0 ? negm : cur[t], 0, 0, 0);
+      // pin the exp chunk to this gap: its input is (opaquely) redefined here and its packed
+      // output consumed here, so no IR pass can hoist or sink it out of the fenced region
+      asm volatile("" : "+v"(prev[et]));
+#pragma unroll
+      for (int j = 0; j < 4; ++j) pf[et][esx][ej + j] = f2bf(__builtin_amdgcn_exp2f(prev[et][8 * esx + ej + j]));
+      asm volatile("" ::"v"(pf[et][esx]));
+      __builtin_amdgcn_sched_barrier(0);
+    });
+    // phase B: PV of tile kt-1 || row max of tile kt
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int sx = 0; sx < 2; ++sx) {
+          asm volatile("" : "+v"(vf[u][t][sx][0]));
+          asm volatile("" : "+v"(vf[u][t][sx][1]));
+        }
+    __builtin_amdgcn_sched_barrier(0);
+    mask_tail(kt, cur);
+    float mxa = -INFINITY, mxb = -INFINITY;
+    __builtin_amdgcn_sched_barrier(0);
+    static_for<0, 12>([&](auto I) {
+      constexpr int i = decltype(I)::value;
+      if constexpr (i < 4) {  // row sums: l^T += ones . P^T
+        lacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ones, pf[i >> 1][i & 1], lacc, 0, 0, 0);
+      } else {                 // O^T += V^T P^T, (u, t, sx) = bits of i - 4
+        constexpr int k = i - 4, u = k >> 2, t = (k >> 1) & 1, sx = k & 1;
+        const uint4 w = make_uint4(vf[u][t][sx][0].x, vf[u][t][sx][0].y, vf[u][t][sx][1].x, vf[u][t][sx][1].y);
+        oacc[u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, w), pf[t][sx], oacc[u], 0, 0, 0);
+      }
+      if constexpr (i < 8) {  // 4 of the 32 scores of tile kt per gap (two v_max3 chains; no
+        // canonicalising v_max x,x pairs as fmaxf would emit)
+        constexpr int t = i >> 2, r = (i & 3) * 4;
+        asm("v_max3_f32 %0, %1, %2, %3" : "=v"(mxa) : "v"(mxa), "v"(cur[t][r]), "v"(cur[t][r + 1]));
+        asm("v_max3_f32 %0, %1, %2, %3" : "=v"(mxb) : "v"(mxb), "v"(cur[t][r + 2]), "v"(cur[t][r + 3]));
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    });
+    float mx = fmaxf(mxa, mxb);
+    mx = fmaxf(mx, xor32(mx));
+    __builtin_amdgcn_sched_barrier(0);
+    if (!__all(mx <= THR)) {  // re-base (rare): after PV(kt-1), before exp of tile kt
+      const float d = fmaxf(mx, 0.f);
+      const float alpha = __builtin_amdgcn_exp2f(-d);
+      m_run += d;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) negm[r] = -m_run;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        oacc[0][r] *= alpha;
+        oacc[1][r] *= alpha;
+        lacc[r] *= alpha;
+      }
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) cur[t][r] -= d;
+    }
+  };
+
+  int kt = 1;
+  for (; kt + 1 < ntile; kt += 2) {
+    step(kt, sB, sA);
+    step(kt + 1, sA, sB);
+  }
+  const bool last_in_b = kt < ntile;
+  if (last_in_b) step(kt, sB, sA);
+  // ---- drain: softmax + PV of the last tile (two static branches: a runtime-selected array
+  // reference would put the S buffers in scratch)
+  auto drain = [&](const f32x16 (&sl)[2]) {
+    uint2 vf[2][2][2][2];
+    vread(ntile - 1, vf);
+    bf16x8 pf[2][2];
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int sx = 0; sx < 2; ++sx)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) pf[t][sx][j] = f2bf(__builtin_amdgcn_exp2f(sl[t][8 * sx + j]));
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int sx = 0; sx < 2; ++sx) {
+          asm volatile("" : "+v"(vf[u][t][sx][0]));
+          asm volatile("" : "+v"(vf[u][t][sx][1]));
+        }
+    __builtin_amdgcn_sched_barrier(0);
+    pv(pf, vf);
+  };
+  if (last_in_b)
+    drain(sB);
+  else
+    drain(sA);
+  const float l_tot = lacc[0];
+  const float inv = l_tot > 0.f ? 1.f / l_tot : 0.f;
+  if (qrow < L) {
+    bf16* O = reinterpret_cast<bf16*>(a.o) + (((int64_t)s_idx * L + qrow) * a.H + head) * 64;
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+      for (int r4 = 0; r4 < 4; ++r4) {
+        bf16x4 w = {f2bf(oacc[u][4 * r4 + 0] * inv), f2bf(oacc[u][4 * r4 + 1] * inv),
+                    f2bf(oacc[u][4 * r4 + 2] * inv), f2bf(oacc[u][4 * r4 + 3] * inv)};
+        *reinterpret_cast<bf16x4*>(O + 32 * u + 8 * r4 + 4 * h) = w;
+      }
+  }
+  probe_exit(a.probe, probe_t);
+}
+
+// ---------------------------------------------------------------- bf16 kernel, v9 (v8 + early K reads)
+// v8 with the LDS reads moved off the tile start: a 5-slot ring three tiles ahead lets the barrier
+// of iteration j publish tile j+1, so the K fragments of tile j+1 are read during the PV MFMAs of
+// iteration j and the V fragments of tile j-1 during the QK MFMAs; no LDS round trip is exposed
+// after a barrier (the v5 stamps measured ~800 cycles per tile there).
+// v2's arithmetic with the softmax of tile j-1 moved under the MFMAs of tile j inside each wave
+// (cdna_hip_programming.md T15; an MFMA holds the SIMD's vector issue for 8 of its 32 cycles,
+// MI355X_MICROARCH.md cycle constants), so the two waves of a SIMD need not take turns:
+//   phase A(j): S_j^T - m = K_j Q^T - m (8 MFMA)   ||  P_{j-1} = bf16(exp2(S_{j-1} - m)) (32 exp + 16 pack)
+//   phase B(j): l += 1 P_{j-1}, O += V_{j-1} P_{j-1} (12 MFMA)  ||  row max of S_j
+//   then the lazy re-base of tile j (rare) and the swap of the two S buffers.
+// K/V tiles of 64 keys ride a 4-slot LDS-DMA ring, two tiles ahead: the V of tile j-1 is read
+// in iteration j, so its slot is refilled only at iteration j+1 (with tile j+3).
+template <bool PRESCALED, int NW>
+__global__ __launch_bounds__(64 * NW, 1) void attn_bf16_v9_kernel(AttnArgs a) {
+  const ProbeT probe_t = probe_enter(a.probe);
+  constexpr int TILE_B = 2 * 64 * 128;  // K + V tile bytes (64 keys x 64 dh bf16 each)
+  constexpr int NS = 5;
+  constexpr int CPW = 512 / (64 * NW);  // 16-B chunks of one K (or V) tile per lane
+  constexpr float THR = 8.f;
+  static_assert(CPW * 64 * NW == 512, "whole DMA rounds");
+  __shared__ __attribute__((aligned(16))) uint4 lds[NS * TILE_B / 16];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int h = lane >> 5;
+  int qb, bh;
+  attn_block(qb, bh);
+  const int s_idx = bh / a.H, head = bh - s_idx * a.H;
+  const int L = a.L;
+  const int64_t base = (int64_t)bh * L * 64;
+  const bf16* Q = reinterpret_cast<const bf16*>(a.q) + base;
+  const bf16* K = reinterpret_cast<const bf16*>(a.k) + base;
+  const bf16* V = reinterpret_cast<const bf16*>(a.v) + base;
+  int klen = L;
+  if (a.kv_len) klen = min(klen, a.kv_len[s_idx]);
+  const int ntile = (klen + 63) / 64;
+
+  const int qrow = qb * (32 * NW) + wid * 32 + (lane & 31);
+  bf16x8 qf[4];
+#pragma unroll
+  for (int ks = 0; ks < 4; ++ks) {
+    uint4 v = *reinterpret_cast<const uint4*>(Q + (int64_t)min(qrow, L - 1) * 64 + ks * 16 + h * 8);
+    qf[ks] = __builtin_bit_cast(bf16x8, v);
+    if constexpr (!PRESCALED) {
+      const float c = a.scale * 1.4426950408889634f;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) qf[ks][j] = f2bf(bf2f(qf[ks][j]) * c);
+    }
+  }
+#pragma unroll
+  for (int ks = 0; ks < 4; ++ks) asm volatile("" ::"v"(qf[ks]));
+
+  int dsrc[CPW];
+#pragma unroll
+  for (int r = 0; r < CPW; ++r) {
+    const int p = (r * NW + wid) * 64 + lane, row = p >> 3, slot = p & 7;
+    dsrc[r] = swz128(row, slot) * 8;
+  }
+  auto dma = [&](int kt) {
+    uint4* Ks = lds + (kt % NS) * (TILE_B / 16);
+    uint4* Vs = Ks + 512;
+#pragma unroll
+    for (int r = 0; r < CPW; ++r) {
+      const int row = ((r * NW + wid) * 64 + lane) >> 3;
+      const int64_t off = (int64_t)min(kt * 64 + row, L - 1) * 64 + dsrc[r];
+      __builtin_amdgcn_global_load_lds((const void*)(K + off), (LDS_PTR(void))(Ks + (r * NW + wid) * 64), 16, 0, 0);
+      __builtin_amdgcn_global_load_lds((const void*)(V + off), (LDS_PTR(void))(Vs + (r * NW + wid) * 64), 16, 0, 0);
+    }
+  };
+
+  const uint32_t lds0 = (uint32_t)(uintptr_t)(LDS_PTR(void))lds;
+  uint32_t kaddr[4];
+#pragma unroll
+  for (int ks = 0; ks < 4; ++ks) {
+    const int row = lane & 31;
+    kaddr[ks] = lds0 + row * 128 + swz128(row, ks * 2 + h) * 16;
+  }
+  const int G = lane >> 4, q4 = (lane & 15) >> 2, p4 = lane & 3;
+  uint32_t vaddr[2][2];
+#pragma unroll
+  for (int u = 0; u < 2; ++u)
+#pragma unroll
+    for (int g8 = 0; g8 < 2; ++g8) {
+      const int r1 = 4 * (G >> 1) + q4 + 8 * g8;
+      const int dh = 32 * u + 16 * (G & 1) + 4 * p4;
+      vaddr[u][g8] = lds0 + 64 * 128 + r1 * 128 + swz128(r1, dh >> 3) * 16 + ((dh >> 2) & 1) * 8;
+    }
+
+  const bf16 one = f2bf(1.f);
+  const bf16x8 ones = {one, one, one, one, one, one, one, one};
+  float m_run = 0.f;
+  f32x16 oacc[2], lacc, sA[2], sB[2];
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    oacc[0][r] = 0.f;
+    oacc[1][r] = 0.f;
+    lacc[r] = 0.f;
+  }
+
+  // K fragments of tile kt (issued and retired here; only LDS op in flight at this point)
+  auto kread = [&](int kt, u32x4 (&kf)[2][4]) {
+    const uint32_t so = (uint32_t)((kt % NS) * TILE_B);
+    static_for<0, 4>([&](auto KS) {
+      constexpr int ks = decltype(KS)::value;
+      kf[0][ks] = lds_b128<0>(kaddr[ks] + so);
+      kf[1][ks] = lds_b128<4096>(kaddr[ks] + so);
+    });
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) asm volatile("" : "+v"(kf[t][ks]));
+  };
+  // V^T fragments of tile kt (retired by the caller's lgkmcnt(0) before the PV MFMAs)
+  auto vread = [&](int kt, uint2 (&vf)[2][2][2][2]) {
+    const uint32_t so = (uint32_t)((kt % NS) * TILE_B);
+    static_for<0, 2>([&](auto U) {
+      constexpr int u = decltype(U)::value;
+      static_for<0, 2>([&](auto T) {
+        constexpr int t = decltype(T)::value;
+        static_for<0, 2>([&](auto S) {
+          constexpr int sx = decltype(S)::value;
+          vf[u][t][sx][0] = lds_tr_b64<(32 * t + 16 * sx) * 128>(vaddr[u][0] + so);
+          vf[u][t][sx][1] = lds_tr_b64<(32 * t + 16 * sx) * 128>(vaddr[u][1] + so);
+        });
+      });
+    });
+  };
+  auto mask_tail = [&](int kt, f32x16 (&sc)[2]) {
+    if (kt * 64 + 64 > klen) {  // ragged last tile: keys past klen get p = 0
+      const int kbase = kt * 64 + 4 * h;
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+          if (kbase + t * 32 + (r & 3) + 8 * (r >> 2) >= klen) sc[t][r] = -INFINITY;
+    }
+  };
+  auto rowmax = [&](const f32x16 (&sc)[2]) {
+    float mx = -INFINITY;
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) mx = fmaxf(mx, sc[t][r]);
+    return fmaxf(mx, xor32(mx));
+  };
+  // PV of the previous tile: l += 1 P^T, O += V^T P^T
+  auto pv = [&](const bf16x8 (&pf)[2][2], uint2 (&vf)[2][2][2][2]) {
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int sx = 0; sx < 2; ++sx) lacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ones, pf[t][sx], lacc, 0, 0, 0);
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int sx = 0; sx < 2; ++sx) {
+          const uint4 w = make_uint4(vf[u][t][sx][0].x, vf[u][t][sx][0].y, vf[u][t][sx][1].x, vf[u][t][sx][1].y);
+          oacc[u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, w), pf[t][sx], oacc[u], 0, 0, 0);
+        }
+  };
+
+  // ---- tile 0: S_0, m_run = its row max (exact first-tile base)
+  dma(0);
+  if (ntile > 1) dma(1);
+  if (ntile > 2) dma(2);
+  if (ntile > 3) dma(3);
+  u32x4 kf[2][4];  // K fragments of the next tile to multiply (loop-carried)
+  {
+    // tiles 0 and 1 visible; 2 and 3 may stay in flight
+    if (ntile > 3)
+      asm volatile("s_waitcnt vmcnt(%0)" ::"i"(4 * CPW) : "memory");
+    else if (ntile > 2)
+      asm volatile("s_waitcnt vmcnt(%0)" ::"i"(2 * CPW) : "memory");
+    else
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    kread(0, kf);
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) sA[t][r] = 0.f;
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks)
+        sA[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, kf[t][ks]), qf[ks], sA[t], 0, 0, 0);
+    }
+    mask_tail(0, sA);
+    m_run = rowmax(sA);
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) sA[t][r] -= m_run;
+    if (ntile > 1) kread(1, kf);
+  }
+
+  // ---- iteration kt >= 1: S_kt into `cur`, softmax + PV of tile kt-1 from `prev`
+  auto step = [&](int kt, f32x16 (&cur)[2], f32x16 (&prev)[2]) {
+    // publish tile kt+1 (its K is read below, during the PV MFMAs); tile kt+2 may stay in flight.
+    // The barrier also retires every wave's reads of tile kt-2's slot, refilled with tile kt+3.
+    if (kt + 1 < ntile) {
+      if (kt + 2 < ntile)
+        asm volatile("s_waitcnt vmcnt(%0)" ::"i"(2 * CPW) : "memory");
+      else
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      if (kt + 3 < ntile) dma(kt + 3);
+    }
+    uint2 vf[2][2][2][2];
+    vread(kt - 1, vf);
+    __builtin_amdgcn_sched_barrier(0);
+    // phase A: QK^T of tile kt || exp/pack of tile kt-1, hand-interleaved (sched_barrier fences):
+    // MFMA (t, ks) alternates the two accumulator chains; each gap carries 4 exp2 + 2 packs.
+    bf16x8 pf[2][2];
+    // K fragments of tile kt were read during the previous iteration: retire them (the V reads
+    // just issued are younger; LDS returns in order, so 16 may stay in flight -> lgkmcnt counts 4 bits)
+    asm volatile("s_waitcnt lgkmcnt(15)" ::: "memory");
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) asm volatile("" : "+v"(kf[t][ks]));
+    __builtin_amdgcn_sched_barrier(0);
+    static_for<0, 8>([&](auto I) {
+      constexpr int i = decltype(I)::value;
+      constexpr int t = i & 1, ks = i >> 1;           // MFMA chain t, k-step ks
+      constexpr int et = i >> 2, esx = (i >> 1) & 1, ej = (i & 1) * 4;  // exp chunk of tile kt-1
+      if constexpr (ks == 0) {  // chain start: C = -m_run broadcast (v_mov, 16 per chain)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) cur[t][r] = -m_run;
+      }
+      cur[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, kf[t][ks]), qf[ks], cur[t], 0, 0, 0);
+      // pin the exp chunk to this gap: its input is (opaquely) redefined here and its packed
+      // output consumed here, so no IR pass can hoist or sink it out of the fenced region
+      asm volatile("" : "+v"(prev[et]));
+#pragma unroll
+      for (int j = 0; j < 4; ++j) pf[et][esx][ej + j] = f2bf(__builtin_amdgcn_exp2f(prev[et][8 * esx + ej + j]));
+      asm volatile("" ::"v"(pf[et][esx]));
+      __builtin_amdgcn_sched_barrier(0);
+    });
+    // phase B: PV of tile kt-1 || row max of tile kt
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int sx = 0; sx < 2; ++sx) {
+          asm volatile("" : "+v"(vf[u][t][sx][0]));
+          asm volatile("" : "+v"(vf[u][t][sx][1]));
+        }
+    __builtin_amdgcn_sched_barrier(0);
+    mask_tail(kt, cur);
+    float mxa = -INFINITY, mxb = -INFINITY;
+    __builtin_amdgcn_sched_barrier(0);
+    static_for<0, 12>([&](auto I) {
+      constexpr int i = decltype(I)::value;
+      if constexpr (i < 4) {  // row sums: l^T += ones . P^T
+        lacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ones, pf[i >> 1][i & 1], lacc, 0, 0, 0);
+      } else {                 // O^T += V^T P^T, (u, t, sx) = bits of i - 4
+        constexpr int k = i - 4, u = k >> 2, t = (k >> 1) & 1, sx = k & 1;
+        const uint4 w = make_uint4(vf[u][t][sx][0].x, vf[u][t][sx][0].y, vf[u][t][sx][1].x, vf[u][t][sx][1].y);
+        oacc[u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, w), pf[t][sx], oacc[u], 0, 0, 0);
+      }
+      if constexpr (i == 5) {  // K fragments of tile kt+1 (published by this iteration's barrier;
+        // past the last tile the read is of a stale slot and unused: no branch, no phi on kf)
+        const uint32_t so = (uint32_t)(((kt + 1) % NS) * TILE_B);
+        static_for<0, 4>([&](auto KS) {
+          constexpr int ks = decltype(KS)::value;
+          kf[0][ks] = lds_b128<0>(kaddr[ks] + so);
+          kf[1][ks] = lds_b128<4096>(kaddr[ks] + so);
+        });
+      }
+      if constexpr (i < 8) {  // 4 of the 32 scores of tile kt per gap (two v_max3 chains; no
+        // canonicalising v_max x,x pairs as fmaxf would emit)
+        constexpr int t = i >> 2, r = (i & 3) * 4;
+        asm("v_max3_f32 %0, %1, %2, %3" : "=v"(mxa) : "v"(mxa), "v"(cur[t][r]), "v"(cur[t][r + 1]));
+        asm("v_max3_f32 %0, %1, %2, %3" : "=v"(mxb) : "v"(mxb), "v"(cur[t][r + 2]), "v"(cur[t][r + 3]));
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    });
+    float mx = fmaxf(mxa, mxb);
+    mx = fmaxf(mx, xor32(mx));
+    __builtin_amdgcn_sched_barrier(0);
+    if (!__all(mx <= THR)) {  // re-base (rare): after PV(kt-1), before exp of tile kt
+      const float d = fmaxf(mx, 0.f);
+      const float alpha = __builtin_amdgcn_exp2f(-d);
+      m_run += d;
+
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        oacc[0][r] *= alpha;
+        oacc[1][r] *= alpha;
+        lacc[r] *= alpha;
+      }
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) cur[t][r] -= d;
+    }
+  };
+
+  int kt = 1;
+  for (; kt + 1 < ntile; kt += 2) {
+    step(kt, sB, sA);
+    step(kt + 1, sA, sB);
+  }
+  const bool last_in_b = kt < ntile;
+  if (last_in_b) step(kt, sB, sA);
+  // ---- drain: softmax + PV of the last tile (two static branches: a runtime-selected array
+  // reference would put the S buffers in scratch)
+  auto drain = [&](const f32x16 (&sl)[2]) {
+    uint2 vf[2][2][2][2];
+    vread(ntile - 1, vf);
+    bf16x8 pf[2][2];
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int sx = 0; sx < 2; ++sx)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) pf[t][sx][j] = f2bf(__builtin_amdgcn_exp2f(sl[t][8 * sx + j]));
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int sx = 0; sx < 2; ++sx) {
+          asm volatile("" : "+v"(vf[u][t][sx][0]));
+          asm volatile("" : "+v"(vf[u][t][sx][1]));
+        }
+    __builtin_amdgcn_sched_barrier(0);
+    pv(pf, vf);
+  };
+  if (last_in_b)
+    drain(sB);
+  else
+    drain(sA);
   const float l_tot = lacc[0];
   const float inv = l_tot > 0.f ? 1.f / l_tot : 0.f;
   if (qrow < L) {
@@ -2143,6 +2865,35 @@ hipError_t attention(int compute, const AttnArgs& a, hipStream_t st) {
       dim3 grid((a.L + 255) / 256, a.S * a.H);
       if (a.prescaled) hipLaunchKernelGGL((attn_bf16_v3_kernel<true>), grid, dim3(512), 0, st, a);
       else hipLaunchKernelGGL((attn_bf16_v3_kernel<false>), grid, dim3(512), 0, st, a);
+      return hipGetLastError();
+    }
+    if (ver == 26) {  // v9: v8 + early K reads (5-slot ring)
+      dim3 grid((a.L + 255) / 256, a.S * a.H);
+      if (a.prescaled) hipLaunchKernelGGL((attn_bf16_v9_kernel<true, 8>), grid, dim3(512), 0, st, a);
+      else hipLaunchKernelGGL((attn_bf16_v9_kernel<false, 8>), grid, dim3(512), 0, st, a);
+      return hipGetLastError();
+    }
+    if (ver == 25) {  // v8: software-pipelined v2
+      dim3 grid((a.L + 255) / 256, a.S * a.H);
+      if (a.prescaled) hipLaunchKernelGGL((attn_bf16_v8_kernel<true, 8>), grid, dim3(512), 0, st, a);
+      else hipLaunchKernelGGL((attn_bf16_v8_kernel<false, 8>), grid, dim3(512), 0, st, a);
+      return hipGetLastError();
+    }
+    if (ver == 23) {  // v2 lean: QK chains start from a -m_run operand, v_max3 row max
+      dim3 grid((a.L + 255) / 256, a.S * a.H);
+      if (a.prescaled) hipLaunchKernelGGL((attn_bf16_v2_kernel<true, 8, 3>), grid, dim3(512), 0, st, a);
+      else hipLaunchKernelGGL((attn_bf16_v2_kernel<false, 8, 3>), grid, dim3(512), 0, st, a);
+      return hipGetLastError();
+    }
+    if (ver == 21 || ver == 22) {  // v2 with wave-priority schedules (measured alternatives)
+      dim3 grid((a.L + 255) / 256, a.S * a.H);
+      if (ver == 21) {
+        if (a.prescaled) hipLaunchKernelGGL((attn_bf16_v2_kernel<true, 8, 1>), grid, dim3(512), 0, st, a);
+        else hipLaunchKernelGGL((attn_bf16_v2_kernel<false, 8, 1>), grid, dim3(512), 0, st, a);
+      } else {
+        if (a.prescaled) hipLaunchKernelGGL((attn_bf16_v2_kernel<true, 8, 2>), grid, dim3(512), 0, st, a);
+        else hipLaunchKernelGGL((attn_bf16_v2_kernel<false, 8, 2>), grid, dim3(512), 0, st, a);
+      }
       return hipGetLastError();
     }
     if (ver == 2 || ver == 24) {

@@ -7,7 +7,7 @@ import statistics
 import sys
 
 sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..", "f5-tts_amd"))
-S, H, N, ROUNDS, REPS = 2, 16, 1876, 6, 10
+S, H, N, ROUNDS, REPS = 2, 16, 1876, int(os.environ.get("AB_ROUNDS", "12")), 10
 
 
 def run(variants):
@@ -15,11 +15,12 @@ def run(variants):
     from f5_tts_amd.engine import attn_force_variant, op_attention
     g = torch.Generator(device="cpu").manual_seed(0)
     Q, K, V = (torch.randn(S, H, N, 64, generator=g).cuda() for _ in range(3))
+    Q = Q * (0.125 * 1.4426950408889634)  # q_prescaled: the engine's layout (scores in log2 units)
     for _ in range(ROUNDS):
         for v in variants:
             attn_force_variant(v)
             for _ in range(REPS):
-                op_attention(Q, K, V, None, compute="bf16")
+                op_attention(Q, K, V, None, compute="bf16", q_prescaled=True)
     torch.cuda.synchronize()
     attn_force_variant(-1)
 
