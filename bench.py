@@ -7,7 +7,7 @@ embedding, 16 packed cond/uncond DiT forwards, CFG + Euler, final cond overwrite
 RCCL all-gather of the finished mels. Synthetic data and hash-PRNG weights of the real
 architecture (checkpoints are network-only).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c3|c5]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c3|c4|c5]
     torchrun --nproc-per-node N bench.py --gpus N ...   (one rank per GPU, weak scaling)
 
 Prints ONE JSON line on rank 0 (contract in the task statement). The default (and the driver's)
@@ -118,7 +118,7 @@ def main():
     ap.add_argument("--compute", default="bf16")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--probe", default="attention", help="kernel class timed live (in-kernel device wall-clock stamps) for the roofline")
-    ap.add_argument("--config", default="c2", choices=("c2", "c3", "c5"),
+    ap.add_argument("--config", default="c2", choices=("c2", "c3", "c4", "c5"),
                     help="workload (SURVEY §8d); c2 is the headline line")
     ap.add_argument("--no-vocos", action="store_true", help="skip the +Vocos decode timing (SURVEY §8f1)")
     ap.add_argument("--probe-all", action="store_true",
@@ -136,7 +136,8 @@ def main():
     device = torch.device("cuda", local)
     torch.cuda.set_device(device)
 
-    case = {"c2": synthetic.c2_case, "c3": synthetic.c3_case, "c5": synthetic.c5_case}[args.config]()
+    case = {"c2": synthetic.c2_case, "c3": synthetic.c3_case, "c4": synthetic.c4_case,
+            "c5": synthetic.c5_case}[args.config]()
     if args.config == "c2":
         case["preset"] = args.preset
     model, arch = build_model(case["preset"], args.compute, device)
@@ -264,6 +265,8 @@ def main():
                   "938 prompt + 938 generated frames (1876), 300 tokens",
             "c3": "C3: F5TTS_v1_Base CFM.sample, NFE 32 linspace + sway -1, CFG 2.0, 32 utterances per GPU, "
                   "564..1876 frames (half prompt), padded to 1876, batch-mask path",
+            "c4": "C4 (per rank): F5TTS_v1_Base CFM.sample, NFE 16 EPSS + sway -1, CFG 2.0, 32 utterances per GPU "
+                  "(256 over 8 GPUs), 938 prompt + 938 generated frames each, 300 tokens, batch path",
             "c5": "C5: E2TTS_Base (UNetT) CFM.sample, NFE 16 EPSS + sway -1, CFG 2.0, 8 utterances per GPU, "
                   "938 prompt + 938 generated frames, 300 tokens",
         }

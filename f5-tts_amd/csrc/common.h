@@ -81,6 +81,13 @@ F5H_DEV float softplus(float x) {  // torch softplus (threshold 20)
   return x > 20.f ? x : log1pf(expf(x));
 }
 F5H_DEV float mish(float x) { return x * tanhf(softplus(x)); }  // nn.Mish, modules.py:181
+// bf16-mode Mish: tanh(log1p(e^x)) = u(u+2) / (u(u+2) + 2), u = e^x (one v_exp + one v_rcp; the
+// x > 20 branch is torch's softplus threshold, where tanh(softplus) == 1 in fp32)
+F5H_DEV float mish_fast(float x) {
+  const float u = __builtin_amdgcn_exp2f(x * 1.4426950408889634f);
+  const float n = u * (u + 2.f);
+  return x > 20.f ? x : x * n * __builtin_amdgcn_rcpf(n + 2.f);
+}
 F5H_DEV float silu(float x) { return x / (1.f + expf(-x)); }
 
 // ---------------------------------------------------------------- wave reductions (64 lanes)

@@ -143,5 +143,11 @@ def c3_case():
                 nt=[max(1, int(t / 6.25)) for t in tot], nfe=32, cfg=2.0, sway=-1.0)
 
 
+def c4_case():
+    """C4 per GPU: 256 utterances of 938 prompt + 938 generated frames over 8 GPUs = 32 per rank
+    (SURVEY §8d), NFE 16 EPSS, CFG 2, batch path (B > 1)."""
+    return dict(preset="F5TTS_v1_Base", B=32, ref=938, total=1876, nt=300, nfe=16, cfg=2.0, sway=-1.0)
+
+
 def c5_case():
     return dict(preset="E2TTS_Base", B=8, ref=938, total=1876, nt=300, nfe=16, cfg=2.0, sway=-1.0)
