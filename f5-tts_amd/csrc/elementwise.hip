@@ -328,22 +328,28 @@ __global__ void grn_sumsq_kernel(const float* x, int S, int L, int C, float* par
   partial[((int64_t)z * S + s) * C + c] = acc;
 }
 // nx[s][c] = Gx / (mean_c Gx + 1e-6), Gx = sqrt(sum_z partial)
-__global__ void grn_norm_kernel(const float* partial, int nz, int S, int C, float* nx) {
+__global__ __launch_bounds__(1024) void grn_norm_kernel(const float* partial, int nz, int S, int C, float* nx) {
+  // one 1024-thread block per sequence, one channel per thread: the nz partials of a channel are
+  // independent loads (kept in flight together), the channel mean is a block reduction
   const int s = blockIdx.x;
   float acc = 0.f;
-  for (int c = threadIdx.x; c < C; c += 256) {
+  for (int c = threadIdx.x; c < C; c += 1024) {
     float ss = 0.f;
+#pragma unroll 8
     for (int z = 0; z < nz; ++z) ss += partial[((int64_t)z * S + s) * C + c];
     const float g = sqrtf(ss);  // ||x||_2 over time
     nx[(int64_t)s * C + c] = g;
     acc += g;
   }
-  __shared__ float red[4];
+  __shared__ float red[16];
   acc = wave_sum(acc);
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
   __syncthreads();
-  const float mean = (red[0] + red[1] + red[2] + red[3]) / C;
-  for (int c = threadIdx.x; c < C; c += 256) nx[(int64_t)s * C + c] = nx[(int64_t)s * C + c] / (mean + 1e-6f);
+  float tot = 0.f;
+#pragma unroll
+  for (int w = 0; w < 16; ++w) tot += red[w];  // fixed order: deterministic
+  const float mean = tot / C;
+  for (int c = threadIdx.x; c < C; c += 1024) nx[(int64_t)s * C + c] = nx[(int64_t)s * C + c] / (mean + 1e-6f);
 }
 template <typename TO>
 __global__ void grn_apply_kernel(const float* x, int L, int C, const float* nx, const float* gamma,
@@ -361,7 +367,7 @@ hipError_t grn(int compute, const float* x, int S, int L, int C, const float* ga
   const int nz = (int)nblk(L, 64);
   float* nx = scratch + (size_t)nz * S * C;
   hipLaunchKernelGGL(grn_sumsq_kernel, dim3(nblk(C, 256), S, nz), dim3(256), 0, st, x, S, L, C, scratch);
-  hipLaunchKernelGGL(grn_norm_kernel, dim3(S), dim3(256), 0, st, scratch, nz, S, C, nx);
+  hipLaunchKernelGGL(grn_norm_kernel, dim3(S), dim3(1024), 0, st, scratch, nz, S, C, nx);
   scratch = nx;
   const int64_t total = (int64_t)S * L * C;
   if (compute)
