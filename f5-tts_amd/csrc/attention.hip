@@ -320,7 +320,10 @@ template <bool PRESCALED, int NW, int PRIO = 0>
 __global__ __launch_bounds__(64 * NW, 1) void attn_bf16_v2_kernel(AttnArgs a) {
   const ProbeT probe_t = probe_enter(a.probe);
   constexpr int TILE_B = 2 * 64 * 128;  // K + V tile bytes (64 keys x 64 dh bf16 each)
-  constexpr int NS = 3;
+  // PRIO 4: one barrier per TWO tiles (6-slot ring, four tiles ahead): halves the per-tile
+  // barrier coupling of the 8 waves (the SQ counters' 32 % wait share)
+  constexpr int TPB = PRIO == 4 ? 2 : 1;
+  constexpr int NS = PRIO == 4 ? 6 : 3;
   constexpr int CPW = 512 / (64 * NW);  // 16-B chunks of one K (or V) tile per lane
   constexpr float THR = 8.f;
   static_assert(CPW * 64 * NW == 512, "whole DMA rounds");
@@ -406,17 +409,37 @@ __global__ __launch_bounds__(64 * NW, 1) void attn_bf16_v2_kernel(AttnArgs a) {
     lacc[r] = 0.f;
   }
 
-  dma(0, 0);
-  if (ntile > 1) dma(1, 1);
+  if constexpr (TPB == 2) {
+    for (int t = 0; t < 4 && t < ntile; ++t) dma(t % NS, t);
+  } else {
+    dma(0, 0);
+    if (ntile > 1) dma(1, 1);
+  }
   if constexpr (PRIO == 1) {
     if (wid >= NW / 2) __builtin_amdgcn_s_setprio(1);
   }
   for (int kt = 0; kt < ntile; ++kt) {
-    if (kt + 1 < ntile)
-      asm volatile("s_waitcnt vmcnt(%0)" ::"i"(2 * CPW) : "memory");
-    else
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
+    if constexpr (TPB == 2) {
+      if ((kt & 1) == 0) {  // tiles kt, kt+1 landed (kt+2, kt+3 may stay in flight), then refill
+        const int ahead = min(ntile - (kt + 2), 2);  // tiles issued after kt+1
+        if (ahead >= 2)
+          asm volatile("s_waitcnt vmcnt(%0)" ::"i"(4 * CPW) : "memory");
+        else if (ahead == 1)
+          asm volatile("s_waitcnt vmcnt(%0)" ::"i"(2 * CPW) : "memory");
+        else
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        // the slots of tiles kt-2, kt-1 were last read before this barrier
+        if (kt + 4 < ntile) dma((kt + 4) % NS, kt + 4);
+        if (kt + 5 < ntile) dma((kt + 5) % NS, kt + 5);
+      }
+    } else {
+      if (kt + 1 < ntile)
+        asm volatile("s_waitcnt vmcnt(%0)" ::"i"(2 * CPW) : "memory");
+      else
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+    }
     const uint32_t so = (uint32_t)((kt % NS) * TILE_B);
 
     u32x4 kf[2][4];
@@ -425,7 +448,9 @@ __global__ __launch_bounds__(64 * NW, 1) void attn_bf16_v2_kernel(AttnArgs a) {
       kf[0][ks] = lds_b128<0>(kaddr[ks] + so);
       kf[1][ks] = lds_b128<4096>(kaddr[ks] + so);
     });
-    if (kt + 2 < ntile) dma((kt + 2) % NS, kt + 2);
+    if constexpr (TPB == 1) {
+      if (kt + 2 < ntile) dma((kt + 2) % NS, kt + 2);
+    }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 #pragma unroll
     for (int t = 0; t < 2; ++t)
@@ -2877,6 +2902,12 @@ hipError_t attention(int compute, const AttnArgs& a, hipStream_t st) {
       dim3 grid((a.L + 255) / 256, a.S * a.H);
       if (a.prescaled) hipLaunchKernelGGL((attn_bf16_v8_kernel<true, 8>), grid, dim3(512), 0, st, a);
       else hipLaunchKernelGGL((attn_bf16_v8_kernel<false, 8>), grid, dim3(512), 0, st, a);
+      return hipGetLastError();
+    }
+    if (ver == 27) {  // v2 with one barrier per two K/V tiles
+      dim3 grid((a.L + 255) / 256, a.S * a.H);
+      if (a.prescaled) hipLaunchKernelGGL((attn_bf16_v2_kernel<true, 8, 4>), grid, dim3(512), 0, st, a);
+      else hipLaunchKernelGGL((attn_bf16_v2_kernel<false, 8, 4>), grid, dim3(512), 0, st, a);
       return hipGetLastError();
     }
     if (ver == 23) {  // v2 lean: QK chains start from a -m_run operand, v_max3 row max

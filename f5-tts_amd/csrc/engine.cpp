@@ -1074,8 +1074,8 @@ int f5h_debug_attn_stamps(uint64_t* out, int32_t n) {
 }
 
 int f5h_attn_force_variant(int32_t v) {
-  if (v != -1 && (v < 1 || v > 9) && v != 21 && v != 22 && v != 23 && v != 24 && v != 25 && v != 26)
-    return fail(F5H_EINVAL, "attention variant must be -1, 1..9, 21..26");
+  if (v != -1 && (v < 1 || v > 9) && (v < 21 || v > 27))
+    return fail(F5H_EINVAL, "attention variant must be -1, 1..9, 21..27");
   attn_force_variant(v);
   g_kernel_epoch.fetch_add(1);
   return 0;

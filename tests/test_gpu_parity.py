@@ -136,7 +136,7 @@ def test_op_attention(compute, tol, S, H, N, masked):
     assert err < tol, err
 
 
-ATTN_VARIANTS = [1, 2, 3, 4, 5, 7, 9, 21, 22, 23, 25, 26]
+ATTN_VARIANTS = [1, 2, 3, 4, 5, 7, 9, 21, 22, 23, 25, 26, 27]
 
 
 @pytest.mark.parametrize("variant", ATTN_VARIANTS)
