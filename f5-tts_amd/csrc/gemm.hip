@@ -533,7 +533,8 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(GemmArgs g) {
     __builtin_amdgcn_sched_barrier(0);
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
-    // ---- mma(p)
+    // ---- mma(p) (ABL 16: s_setprio 1 around the MFMA cluster, guide T5 — measurement variant)
+    if constexpr ((ABL & 16) != 0) __builtin_amdgcn_s_setprio(1);
     if constexpr (!(ABL & 2))
 #pragma unroll
     for (int s = 0; s < KS; ++s)
@@ -543,6 +544,7 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(GemmArgs g) {
         for (int j = 0; j < NT; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, af[s][i]),
                                                               __builtin_bit_cast(bf16x8, bfr[s][j]), acc[i][j], 0, 0, 0);
+    if constexpr ((ABL & 16) != 0) __builtin_amdgcn_s_setprio(0);
     __builtin_amdgcn_sched_barrier(0);
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
@@ -604,6 +606,7 @@ static void launch_pp(const GemmArgs& a, hipStream_t st) {
       case 7: F5H_PP(7); return;
       case 8: F5H_PP(8); return;
       case 15: F5H_PP(15); return;
+      case 16: F5H_PP(16); return;
       default: break;
     }
   }

@@ -21,6 +21,10 @@ CFGS = {0: (64, 128, 256), 1: (128, 128, 256), 2: (128, 256, 512), 3: (192, 256,
         10: (256, 256, 512), 11: (256, 192, 512), 12: (256, 128, 512), 13: (128, 128, 512), 14: (128, 128, 512),
         15: (256, 64, 512), 16: (128, 256, 512), 17: (256, 256, 512)}
 REPS = 20
+if os.environ.get("GT_CFGS"):  # e.g. GT_CFGS=5,11 GT_SHAPES=c3_qkv,c3_ffn2
+    CFGS = {int(c): CFGS[int(c)] for c in os.environ["GT_CFGS"].split(",")}
+if os.environ.get("GT_SHAPES"):
+    SHAPES = {k: SHAPES[k] for k in os.environ["GT_SHAPES"].split(",")}
 
 
 def grid_threads(M, N, cfg):
