@@ -314,3 +314,51 @@ def test_step_graph_bitwise_equals_eager(name):
     o_c, _ = run(cfg_strength=cfg + 0.5)
     assert eng.graph_stats()["captures"] == s2["captures"] + 1
     assert not torch.equal(o_c, o_e)
+
+
+def test_concurrent_samples_on_two_streams_match_sequential():
+    """The reference samples from a ThreadPoolExecutor (utils_infer.py:540-541). Two host threads,
+    each on its own stream and with its own inputs, sampling repeatedly through one engine (step
+    graphs on): every result equals the sequential one bit for bit."""
+    _need_gpu()
+    import threading
+
+    tag, spec, nfe, sway, cfg = gc.SAMPLE_CASES["dit_tiny_sample_b3"]
+    arch = gc.arch_of(tag)
+    m = _model(arch, "bf16")
+    cases = []
+    for seed in (1, 2):
+        inp = synthetic.make_case(**spec, seed=seed)
+        dur = torch.maximum(torch.maximum((inp["text"] != -1).sum(-1), inp["lens"]) + 1, inp["duration"])
+        cases.append((inp, synthetic.reference_noise(dur, seed)))
+
+    def run(inp, y0):
+        out, _ = m.sample(cond=inp["cond"].to(DEV), text=inp["text"].to(DEV), duration=inp["duration"].to(DEV),
+                          lens=inp["lens"].to(DEV), steps=nfe, cfg_strength=cfg, sway_sampling_coef=sway,
+                          y0=y0.to(DEV), keep_trajectory=False)
+        return out
+
+    ref = [run(*c).clone() for c in cases]
+    torch.cuda.synchronize()
+    results, errors = [[], []], []
+
+    def worker(i):
+        try:
+            s = torch.cuda.Stream()
+            with torch.cuda.stream(s):
+                for _ in range(4):
+                    results[i].append(run(*cases[i]).clone())
+            s.synchronize()
+        except Exception as ex:  # surfaced below
+            errors.append(ex)
+
+    ts = [threading.Thread(target=worker, args=(i,)) for i in range(2)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join(timeout=120)
+    assert not errors, errors
+    for i in range(2):
+        assert len(results[i]) == 4
+        for r in results[i]:
+            assert torch.equal(r, ref[i])
