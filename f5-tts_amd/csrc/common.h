@@ -34,12 +34,28 @@ F5H_DEV float gelu_tanh(float x) {  // nn.GELU(approximate="tanh"), modules.py:3
   float u = k0 * (x + k1 * x * x * x);
   return 0.5f * x * (1.f + tanhf(u));
 }
+// Uncontracted fp32 ops (the build uses -ffp-contract=fast-honor-pragmas): epilogue arithmetic
+// that must round identically in every kernel that inlines it (bitwise-identical tile configs).
+F5H_DEV float mul_nc(float a, float b) {
+#pragma clang fp contract(off)
+  return a * b;
+}
+F5H_DEV float add_nc(float a, float b) {
+#pragma clang fp contract(off)
+  return a + b;
+}
+F5H_DEV float sub_nc(float a, float b) {
+#pragma clang fp contract(off)
+  return a - b;
+}
+
 // bf16-mode form: 0.5x(1+tanh(u)) == x * sigmoid(2u) = x / (1 + 2^(-2u*log2 e)); v_exp_f32 + v_rcp_f32
 // (rel. error ~1e-6, far below the bf16 rounding of the result; the fp32 parity mode keeps tanhf)
-F5H_DEV float gelu_tanh_fast(float x) {
+F5H_DEV float gelu_tanh_fast(float x) {  // explicit rounding: identical in every kernel that inlines it
   const float k0 = 0.7978845608028654f * 2.f * 1.4426950408889634f, k1 = 0.044715f;
-  const float u = k0 * (x + k1 * x * x * x);
-  return x * __builtin_amdgcn_rcpf(1.f + __builtin_amdgcn_exp2f(-u));
+  const float x3 = mul_nc(mul_nc(x, x), x);
+  const float u = mul_nc(k0, add_nc(x, mul_nc(k1, x3)));
+  return mul_nc(x, __builtin_amdgcn_rcpf(add_nc(1.f, __builtin_amdgcn_exp2f(-u))));
 }
 // ---------------------------------------------------------------- in-kernel launch probe
 // Kernel-side timing of probed launches (f5h_probe_*): the first thread of every workgroup
@@ -74,8 +90,8 @@ F5H_DEV void probe_exit(const f5h::DevProbe& p, const ProbeT& r) {
   }
 }
 
-F5H_DEV float gelu_erf(float x) {  // nn.GELU(), modules.py:266
-  return 0.5f * x * (1.f + erff(x * 0.7071067811865476f));
+F5H_DEV float gelu_erf(float x) {  // nn.GELU(), modules.py:266 (explicit rounding, see gelu_tanh_fast)
+  return mul_nc(mul_nc(0.5f, x), add_nc(1.f, erff(mul_nc(x, 0.7071067811865476f))));
 }
 F5H_DEV float softplus(float x) {  // torch softplus (threshold 20)
   return x > 20.f ? x : log1pf(expf(x));

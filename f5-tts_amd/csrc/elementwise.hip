@@ -444,17 +444,17 @@ __global__ void cfg_euler_kernel(EulerArgs a, TO* ypad) {
   float v = pc;
   if (a.use_cfg) {
     const float pu = a.p[(int64_t)(a.B + b) * a.p_seq_stride + (int64_t)(a.p_row_off + n) * a.p_ld + c];
-    v = __fadd_rn(pc, __fmul_rn(__fsub_rn(pc, pu), a.cfg));
+    v = add_nc(pc, mul_nc(sub_nc(pc, pu), a.cfg));
   }
   float dt = a.dt;
   float* traj = a.traj;
   if (a.kstep) {  // graph-replayable form: step index, grid and trajectory base live on the device
     const int k = *a.kstep;
-    dt = __fsub_rn(a.tgrid[k + 1], a.tgrid[k]);
+    dt = sub_nc(a.tgrid[k + 1], a.tgrid[k]);
     traj = a.trajp ? *a.trajp : nullptr;
     if (traj) traj += (int64_t)(k + 1) * total;
   }
-  const float y = __fadd_rn(a.y[i], __fmul_rn(dt, v));
+  const float y = add_nc(a.y[i], mul_nc(dt, v));
   a.y[i] = y;
   if (ypad) ypad[bn * 128 + c] = from_f32<TO>(y);
   if (traj) traj[i] = y;

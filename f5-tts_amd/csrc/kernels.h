@@ -47,6 +47,7 @@ struct GemmArgs {
   void* q; void* k; void* v;
   float q_scale;                   // EPI_QKV: q is stored pre-multiplied by this (0 -> 1)
   DevProbe probe;                  // in-kernel launch timing (null slots: off)
+  int diag_skip_epilogue;          // diagnostics only (F5H_GEMM_DIAG=1): no epilogue, results invalid
 };
 
 // compute: 0 fp32 operands, 1 bf16 operands. A and W both in the operand dtype.
