@@ -211,8 +211,9 @@ def dit_block(W, i, arch, x, t_emb, mask, rope):
     return x + g2[:, None] * ffn(W, p + "ff.", f)
 
 
-def dit_forward(W, arch, x, cond, text, t, mask, text_cache):
-    """Packed cond/uncond DiT forward (cfg_infer=True, cache=True). Returns [2b,n,mel]."""
+def dit_forward(W, arch, x, cond, text, t, mask, text_cache, packed=True):
+    """Packed cond/uncond DiT forward (cfg_infer=True, cache=True). Returns [2b,n,mel].
+    `packed=False`: the single conditional forward of `cfm.py:167-178` (drop flags False) -> [b,n,mel]."""
     b, n = x.shape[:2]
     t = t.reshape(-1).expand(b) if t.numel() == 1 else t
     te = time_embed(W, t)
@@ -221,10 +222,13 @@ def dit_forward(W, arch, x, cond, text, t, mask, text_cache):
         text_cache["cond"] = text_embed_dit(W, arch, text, seq, False)
         text_cache["uncond"] = text_embed_dit(W, arch, text, seq, True)
     xc = input_embed(W, x, cond, text_cache["cond"], False, mask)
-    xu = input_embed(W, x, cond, text_cache["uncond"], True, mask)
-    h = torch.cat((xc, xu), 0)
-    te = torch.cat((te, te), 0)
-    m2 = None if mask is None else torch.cat((mask, mask), 0)
+    if packed:
+        xu = input_embed(W, x, cond, text_cache["uncond"], True, mask)
+        h = torch.cat((xc, xu), 0)
+        te = torch.cat((te, te), 0)
+        m2 = None if mask is None else torch.cat((mask, mask), 0)
+    else:
+        h, m2 = xc, mask
     rope = rope_cos_sin(n, arch["dim_head"])
     for i in range(arch["depth"]):
         h = dit_block(W, i, arch, h, te, m2, rope)
@@ -249,7 +253,7 @@ def text_embed_unett(W, arch, text, n, drop_text):
     return W["text_embed.text_embed.weight"][text]  # conv_layers=0 for E2 Base
 
 
-def unett_forward(W, arch, x, cond, text, t, mask, text_cache):
+def unett_forward(W, arch, x, cond, text, t, mask, text_cache, packed=True):
     b, n = x.shape[:2]
     t = t.reshape(-1).expand(b) if t.numel() == 1 else t
     te = time_embed(W, t)
@@ -257,10 +261,13 @@ def unett_forward(W, arch, x, cond, text, t, mask, text_cache):
         text_cache["cond"] = text_embed_unett(W, arch, text, n, False)
         text_cache["uncond"] = text_embed_unett(W, arch, text, n, True)
     xc = input_embed(W, x, cond, text_cache["cond"], False, None)  # no mask (unett.py:90-102)
-    xu = input_embed(W, x, cond, text_cache["uncond"], True, None)
-    h = torch.cat((xc, xu), 0)
-    te = torch.cat((te, te), 0)
-    m2 = None if mask is None else torch.cat((mask, mask), 0)
+    if packed:
+        xu = input_embed(W, x, cond, text_cache["uncond"], True, None)
+        h = torch.cat((xc, xu), 0)
+        te = torch.cat((te, te), 0)
+        m2 = None if mask is None else torch.cat((mask, mask), 0)
+    else:
+        h, m2 = xc, mask
     h = torch.cat((te[:, None], h), 1)
     if m2 is not None:
         m2 = F.pad(m2, (1, 0), value=True)
@@ -281,7 +288,7 @@ def unett_forward(W, arch, x, cond, text, t, mask, text_cache):
 
 # ------------------------------------------------------------------ sampler
 
-def prepare(arch, cond, text, duration, lens=None, max_duration=65536, edit_mask=None):
+def prepare(arch, cond, text, duration, lens=None, max_duration=65536, edit_mask=None, no_ref_audio=False):
     """The host-side preamble of CFM.sample (cfm.py:111-158). Returns a dict."""
     B, cond_len = cond.shape[:2]
     if lens is None:
@@ -295,6 +302,8 @@ def prepare(arch, cond, text, duration, lens=None, max_duration=65536, edit_mask
     duration = duration.clamp(max=max_duration)
     N = int(duration.max())
     cond = F.pad(cond, (0, 0, 0, N - cond_len), value=0.0)
+    if no_ref_audio:  # cfm.py:146-147
+        cond = torch.zeros_like(cond)
     cond_mask = F.pad(cond_mask, (0, N - cond_mask.shape[-1]), value=False)[..., None]
     step_cond = torch.where(cond_mask, cond, torch.zeros_like(cond))
     mask = lens_to_mask(duration) if B > 1 else None
@@ -304,10 +313,10 @@ def prepare(arch, cond, text, duration, lens=None, max_duration=65536, edit_mask
 @torch.no_grad()
 def cfm_sample(W, arch, cond, text, duration, *, lens=None, steps=32, cfg_strength=1.0,
                sway_sampling_coef=None, y0=None, seed=None, use_epss=True, edit_mask=None,
-               max_steps=None):
+               max_steps=None, no_ref_audio=False):
     """fp32 restatement of CFM.sample. `y0` overrides the noise recipe (cfm.py:196-201).
     `max_steps` truncates the Euler loop (used only for bounded CPU-baseline timing)."""
-    pre = prepare(arch, cond.float(), text, duration, lens, edit_mask=edit_mask)
+    pre = prepare(arch, cond.float(), text, duration, lens, edit_mask=edit_mask, no_ref_audio=no_ref_audio)
     if y0 is None:
         from torch.nn.utils.rnn import pad_sequence
         ys = []
@@ -320,8 +329,8 @@ def cfm_sample(W, arch, cond, text, duration, *, lens=None, steps=32, cfg_streng
     cache = {}
 
     def fn(t, x):
-        if cfg_strength < 1e-5:
-            raise NotImplementedError("oracle restates the CFG path (cfg_strength >= 1e-5) only")
+        if cfg_strength < 1e-5:  # cfm.py:167-178: one conditional forward, no guidance
+            return fwd(W, arch, x, pre["step_cond"], text, t, pre["mask"], cache, packed=False)
         p = fwd(W, arch, x, pre["step_cond"], text, t, pre["mask"], cache)
         pc, pu = torch.chunk(p, 2, 0)
         return pc + (pc - pu) * cfg_strength

@@ -167,6 +167,20 @@ def run_sample(arch, case, nfe, cfg=2.0, sway=-1.0, dtype=torch.float32, seed=7,
     return out.float().numpy(), traj.float().numpy(), inp
 
 
+def run_edge(name, seed=7):
+    """One golden_cases.EDGE_CASES entry through the reference CFM.sample."""
+    import golden_cases as gc
+
+    tag, case, nfe, sway, cfg, extra = gc.EDGE_CASES[name]
+    model = build_ref(gc.arch_of(tag))
+    inp = synthetic.make_case(**case)
+    kw = gc.edge_sample_kwargs(inp, extra)
+    with fp32_noise(), torch.no_grad():
+        out, traj = model.sample(**kw, steps=nfe, cfg_strength=cfg, sway_sampling_coef=sway, seed=seed)
+    return dict(out=out.float().numpy(), traj_last=traj[-1].float().numpy(), traj_1=traj[1].float().numpy(),
+                checksum=checksum(inp))
+
+
 def run_forward(arch, case, t_val=0.3, seed=7):
     """One packed cond/uncond backbone forward at time t (dit.py:319-370 with cfg_infer=True)."""
     model = build_ref(arch)
@@ -229,6 +243,11 @@ def main():
     c1_case = dict(B=1, ref_frames=282, total_frames=564, n_text=90)
     for dt, tag in ((torch.float32, "fp32"), (torch.bfloat16, "bf16"), (torch.float16, "fp16")):
         jobs[f"c1_sample_{tag}"] = sample_job(c1, c1_case, 4, dtype=dt)
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))  # tests/
+    import golden_cases as gc
+
+    for name in gc.EDGE_CASES:
+        jobs[name] = (lambda n: (lambda: run_edge(n)))(name)
     if not args.skip_c2:
         c2 = configs.get_arch("F5TTS_v1_Base")
         jobs["c2_sample_fp32"] = sample_job(c2, dict(B=1, ref_frames=938, total_frames=1876, n_text=300), 16)

@@ -79,3 +79,46 @@ def max_rel(a, b):
     a = np.asarray(a, dtype=np.float64)
     b = np.asarray(b, dtype=np.float64)
     return float(np.abs(a - b).max() / max(np.abs(b).max(), 1e-30))
+
+
+# Edge cases of CFM.sample's host preamble and ODE loop (reference cfm.py:83-229), each produced by
+# the reference itself (tests/golden/make_golden.py --only edge):
+# name -> (arch tag, input spec, nfe, sway, cfg, extra)
+#   extra: edit     -> edit_mask [B, cond_len] with a False span [lens//3, lens//2) (speech_edit.py path)
+#          no_ref   -> no_ref_audio=True (cfm.py:146-147)
+#          int_dur  -> duration passed as a python int (cfm.py:132-139 rule then lifts it per utterance)
+#          epss     -> use_epss flag
+SHORT = dict(B=1, ref_frames=3, total_frames=5, n_text=2, vocab=64)
+EDGE_CASES = {
+    "edge_dit_nocfg_b1": ("tiny", B1, 4, -1.0, 0.0, {}),
+    "edge_dit_nocfg_b3": ("tiny", B3, 3, -1.0, 0.0, {}),
+    "edge_unett_nocfg_b3": ("utiny", B3, 3, -1.0, 0.0, {}),
+    "edge_dit_edit_b3": ("tiny", B3, 4, -1.0, 2.0, {"edit": True}),
+    "edge_dit_noref_b1": ("tiny", B1, 4, -1.0, 2.0, {"no_ref": True}),
+    "edge_dit_intdur_b3": ("tiny", B3, 2, -1.0, 2.0, {"int_dur": 10}),
+    "edge_dit_nfe1_b1": ("tiny", B1, 1, None, 2.0, {}),
+    "edge_dit_short_b1": ("tiny", SHORT, 3, -1.0, 2.0, {}),
+    "edge_dit_lin7_b3": ("tiny", B3, 7, 0.5, 1.5, {"epss": False}),
+}
+
+
+def edit_mask_for(lens, cond_len):
+    """[B, cond_len] bool: True except [lens//3, lens//2) per utterance."""
+    import torch
+
+    ar = torch.arange(cond_len)[None]
+    lo, hi = (lens // 3)[:, None], (lens // 2)[:, None]
+    return ~((ar >= lo) & (ar < hi))
+
+
+def edge_sample_kwargs(inp, extra):
+    """The CFM.sample keyword arguments of an edge case (inputs from synthetic.make_case)."""
+    kw = dict(cond=inp["cond"], text=inp["text"], lens=inp["lens"],
+              duration=extra.get("int_dur", inp["duration"]))
+    if extra.get("edit"):
+        kw["edit_mask"] = edit_mask_for(inp["lens"], inp["cond"].shape[1])
+    if extra.get("no_ref"):
+        kw["no_ref_audio"] = True
+    if "epss" in extra:
+        kw["use_epss"] = extra["epss"]
+    return kw

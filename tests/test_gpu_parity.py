@@ -214,6 +214,34 @@ def test_sample_fp32_matches_reference(name):
     assert e < FP32_TOL, e
 
 
+@pytest.mark.parametrize("compute", ["fp32", "bf16"])
+@pytest.mark.parametrize("name", list(gc.EDGE_CASES))
+def test_edge_sample_matches_reference(name, compute):
+    """Edge paths of CFM.sample against the reference's own outputs: cfg=0 (one conditional forward,
+    S=B), edit mask, no_ref_audio, int duration lifted by the duration rule, NFE 1, a 5-frame
+    sequence, linspace grid with positive sway. fp32: max-rel <= 1e-3; bf16: rel-L2 <= 5e-2."""
+    _need_gpu()
+    g = gc.load(name)
+    tag, spec, nfe, sway, cfg, extra = gc.EDGE_CASES[name]
+    arch = gc.arch_of(tag)
+    m = _model(arch, compute)
+    inp = synthetic.make_case(**spec)
+    kw = gc.edge_sample_kwargs(inp, extra)
+    dur = torch.as_tensor(kw["duration"]).expand(inp["lens"].shape[0])
+    dur = torch.maximum(torch.maximum((inp["text"] != -1).sum(-1), inp["lens"]) + 1, dur)
+    y0 = synthetic.reference_noise(dur, gc.SEED)
+    kw = {k: (v.to(DEV) if isinstance(v, torch.Tensor) else v) for k, v in kw.items()}
+    out, traj = m.sample(**kw, steps=nfe, cfg_strength=cfg, sway_sampling_coef=sway, y0=y0.to(DEV))
+    torch.cuda.synchronize()
+    out = out.float().cpu().numpy()
+    assert out.shape == g["out"].shape
+    if compute == "fp32":
+        assert gc.max_rel(traj[1].float().cpu().numpy(), g["traj_1"]) < FP32_TOL
+        assert gc.max_rel(out, g["out"]) < FP32_TOL
+    else:
+        assert gc.rel_err(out, g["out"]) < 5e-2
+
+
 def test_sample_bf16_within_reference_bf16_envelope_c1():
     """engine-bf16 error vs reference-fp32 <= 1.5x reference-bf16 error vs reference-fp32."""
     _need_gpu()

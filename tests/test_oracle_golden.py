@@ -53,6 +53,24 @@ def test_oracle_sample_matches_reference(name, torch_threads):
     assert gc.max_rel(out.numpy(), g["out"]) < SAMPLE_TOL
 
 
+@pytest.mark.parametrize("name", list(gc.EDGE_CASES))
+def test_oracle_edge_sample_matches_reference(name, torch_threads):
+    """cfg=0 single forward, edit mask, no_ref_audio, int duration, NFE 1, 5-frame sequence,
+    linspace grid with positive sway: the reference's own outputs."""
+    g = gc.load(name)
+    assert g is not None, f"missing fixture {name}"
+    tag, spec, nfe, sway, cfg, extra = gc.EDGE_CASES[name]
+    arch = gc.arch_of(tag)
+    W = synthetic.make_weights_torch(arch)
+    inp = _inputs(spec)
+    kw = gc.edge_sample_kwargs(inp, extra)
+    out, traj = ref_cpu.cfm_sample(W, arch, kw.pop("cond"), kw.pop("text"), kw.pop("duration"), steps=nfe,
+                                   cfg_strength=cfg, sway_sampling_coef=sway, seed=gc.SEED, **kw)
+    assert out.shape == g["out"].shape
+    assert gc.max_rel(traj[1].numpy(), g["traj_1"]) < SAMPLE_TOL
+    assert gc.max_rel(out.numpy(), g["out"]) < SAMPLE_TOL
+
+
 def test_time_grids_match_reference():
     g = gc.load("time_grids")
     for n in (4, 5, 6, 7, 10, 12, 16, 32):
