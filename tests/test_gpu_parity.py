@@ -390,3 +390,29 @@ def test_concurrent_samples_on_two_streams_match_sequential():
         assert len(results[i]) == 4
         for r in results[i]:
             assert torch.equal(r, ref[i])
+
+
+def test_maximum_length_matches_oracle_and_beyond_raises():
+    """N = 8192, the reference's text position table (precompute_max_pos, dit.py:47): fp32 engine
+    vs the CPU oracle within 1e-3 (DiT_tiny, 2 Euler steps); one frame more raises, as the
+    reference's freqs_cis[:N] broadcast would."""
+    _need_gpu()
+    from oracle import ref_cpu
+
+    arch = gc.arch_of("tiny")
+    W = synthetic.make_weights_torch(arch)
+    m = _model(arch, "fp32")
+    inp = synthetic.make_case(B=1, ref_frames=4000, total_frames=8192, n_text=900, vocab=64)
+    dur = torch.maximum(torch.maximum((inp["text"] != -1).sum(-1), inp["lens"]) + 1, inp["duration"])
+    y0 = synthetic.reference_noise(dur, gc.SEED)
+    kw = dict(steps=2, cfg_strength=2.0, sway_sampling_coef=-1.0)
+    with torch.no_grad():
+        ref, _ = ref_cpu.cfm_sample(W, arch, inp["cond"], inp["text"], inp["duration"], lens=inp["lens"], y0=y0, **kw)
+    out, _ = m.sample(cond=inp["cond"].to(DEV), text=inp["text"].to(DEV), duration=inp["duration"].to(DEV),
+                      lens=inp["lens"].to(DEV), y0=y0.to(DEV), keep_trajectory=False, **kw)
+    torch.cuda.synchronize()
+    assert out.shape == (1, 8192, 100)
+    assert gc.max_rel(out.float().cpu().numpy(), ref.numpy()) < FP32_TOL
+    with pytest.raises(RuntimeError):
+        m.sample(cond=inp["cond"].to(DEV), text=inp["text"].to(DEV), duration=8193, lens=inp["lens"].to(DEV),
+                 keep_trajectory=False, **kw)
