@@ -259,6 +259,8 @@ def main():
 
     # whole-path algorithmic FLOPs: NFE * S * F(N) at the padded length
     flops_call = case["nfe"] * S * seq_flops(arch, Nmax)
+    # useful work of a mixed-length batch: each utterance at its own length
+    useful_call = case["nfe"] * (S // B) * sum(seq_flops(arch, t) for t in tots)
     if rank == 0:
         workloads = {
             "c2": "C2: F5TTS_v1_Base CFM.sample, NFE 16 EPSS + sway -1, CFG 2.0, 1 utterance per GPU, "
@@ -287,6 +289,7 @@ def main():
                        "gen_frames": gen_frames, "nfe": case["nfe"], "parallelism": f"dp{world}"},
             "rtf": round(rtf, 5),
             "path_tflops": round(flops_call * args.steps * world / elapsed / 1e12, 2),
+            "path_tflops_useful": round(useful_call * args.steps * world / elapsed / 1e12, 2),
             "roofline": roof,
             "vocos": vocos,
             "cpu_baseline": cpu,
