@@ -1,0 +1,37 @@
+"""The algorithmic FLOP counts behind bench.py's `path_tflops` and `roofline.achieved`, against the
+figures SURVEY §8(d) derives from the reference's shapes (and thop's count, count_params_gflops.py)."""
+
+import pytest
+
+import bench
+from f5_tts_amd import configs
+
+
+def test_dit_base_sequence_forward_matches_survey():
+    arch = configs.get_arch("F5TTS_v1_Base")
+    n = 1876
+    survey = 378.888e6 * n + 90112.0 * n * n  # F(N), SURVEY §8(d)
+    assert bench.seq_flops(arch, n) == pytest.approx(survey, rel=1e-4)
+    assert bench.seq_flops(arch, n) == pytest.approx(1027.9e9, rel=1e-3)
+    # per NFE step (S = 2 with CFG) and per C2 call (NFE 16)
+    assert 2 * bench.seq_flops(arch, n) == pytest.approx(2.056e12, rel=1e-3)
+    assert 16 * 2 * bench.seq_flops(arch, n) == pytest.approx(32.89e12, rel=1e-3)
+
+
+def test_e2_unett_sequence_forward_matches_survey():
+    arch = configs.get_arch("E2TTS_Base")
+    assert bench.seq_flops(arch, 1876) == pytest.approx(1591.3e9, rel=2e-3)
+    attn = 4.0 * arch["depth"] * arch["dim"] * 1877 ** 2  # UNetT attends over N + 1 (time token)
+    assert attn == pytest.approx(346.3e9, rel=2e-3)
+
+
+def test_probe_class_flops():
+    arch = configs.get_arch("F5TTS_v1_Base")
+    S, L = 2, 1876
+    assert bench.attn_flops(S, arch["heads"], L) == pytest.approx(28.83e9, rel=1e-3)
+    assert bench.class_flops("attention", arch, S, L) == bench.attn_flops(S, arch["heads"], L)
+    assert bench.class_flops("qkv", arch, S, L) == pytest.approx(23.6e9, rel=2e-3)
+    assert bench.class_flops("out", arch, S, L) == pytest.approx(7.87e9, rel=2e-3)
+    assert bench.class_flops("ffn1", arch, S, L) == pytest.approx(15.7e9, rel=3e-3)
+    assert bench.class_flops("conv", arch, S, L) == pytest.approx(15.26e9, rel=3e-3)
+    assert bench.class_flops("norm", arch, S, L) == 0.0  # HBM-bound: no FLOP roofline
