@@ -2,17 +2,20 @@
 
 Workload (BASELINE.json configs[1] = SURVEY C2): F5TTS_v1_Base, bf16 MFMA engine, NFE 16
 (EPSS grid) + sway -1, CFG 2.0, B=1 per GPU, 10 s prompt (938 ref frames) + 938 generated
-frames = 1876 frames, 300 text tokens. One "step" = one full `CFM.sample()` call (text
-embedding, 16 packed cond/uncond DiT forwards, CFG + Euler, final cond overwrite) plus the
-RCCL all-gather of the finished mels. Synthetic data and hash-PRNG weights of the real
-architecture (checkpoints are network-only).
+frames = 1876 frames, 300 text tokens. One "step" = one pass of the data-parallel job driver
+(f5_tts_amd.parallel.run_sharded: LPT shard -> length buckets -> CFM.sample per batch -> keep the
+generated frames -> RCCL gather of the finished mels when N > 1), i.e. one full `CFM.sample()` per
+GPU at C2. Synthetic data and hash-PRNG weights of the real architecture (checkpoints are
+network-only); inputs are resident on the device before the timed region.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c3|c4|c5]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c3|c4|c5] [--compute bf16|fp16]
     torchrun --nproc-per-node N bench.py --gpus N ...   (one rank per GPU, weak scaling)
 
-Prints ONE JSON line on rank 0 (contract in the task statement). The default (and the driver's)
-workload is C2; --config c3 (B=32 mixed lengths, NFE 32, batch-mask path) and c5 (E2 UNetT,
-B=8) measure the other BASELINE.json configs the same way (no CPU baseline for those).
+Prints ONE JSON line on rank 0 (contract in the task statement). `roofline` is the kernel class that
+takes the most time per step (in-kernel device wall-clock stamps, probed live over the timed region);
+`roofline_classes` lists every class from a probe pre-pass. The default (and the driver's) workload
+is C2; --config c3 (B=32 mixed lengths, NFE 32, batch-mask path), c4 (32 utterances per GPU) and c5
+(E2 UNetT, B=8) measure the other BASELINE.json configs the same way (no CPU baseline for those).
 """
 
 from __future__ import annotations
@@ -54,15 +57,19 @@ def seq_flops(arch, N):
 
 
 def pmc_traffic(kernel_class):
-    """HBM bytes per launch of the probed kernel from the committed rocprofv3 PMC summary
-    (profiles/*_pmc_<class>.json, written by tools/profile_round.sh): FETCH_SIZE doubled (it
-    reads 1/2 of wide streaming reads on gfx950, MI355X_MICROARCH.md §HBM) + WRITE_SIZE."""
+    """HBM bytes per launch of a kernel class from the latest committed rocprofv3 PMC summary
+    (profiles/*_pmc_classes.json, written by tools/pmc_classes.py from separate FETCH_SIZE and
+    WRITE_SIZE passes: 2 x FETCH_SIZE (gfx950 counts half of wide streaming reads,
+    MI355X_MICROARCH.md §HBM) + WRITE_SIZE), and its source file."""
     import glob
-    files = sorted(glob.glob(os.path.join(REPO, "profiles", f"*_pmc_{kernel_class}.json")))
+    files = sorted(glob.glob(os.path.join(REPO, "profiles", "*_pmc_classes.json")))
     if not files:
         return None, None
     d = json.load(open(files[-1]))
-    return (2.0 * d["fetch_size_kb"] + d["write_size_kb"]) * 1024.0, os.path.relpath(files[-1], REPO)
+    ent = d.get("classes", {}).get(kernel_class)
+    if not ent:
+        return None, os.path.relpath(files[-1], REPO)
+    return ent["hbm_bytes"], os.path.relpath(files[-1], REPO)
 
 
 def build_model(preset, compute, device):
@@ -77,28 +84,34 @@ def build_model(preset, compute, device):
     return CFM(transformer=net, num_channels=100, compute=compute).to(device), arch
 
 
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
 def cpu_baseline(case, arch, threads):
-    """Oracle (fp32 PyTorch-CPU restatement) on a bounded sample of the same workload:
-    1 and 3 Euler steps of the C2 call; full-call time extrapolated as prologue + NFE x step."""
+    """Oracle (fp32 PyTorch-CPU restatement of the reference path) timed on the host cores: one full
+    16-step C2 CFM.sample call (text embedding, 16 packed CFG forwards, Euler, final overwrite)."""
     from f5_tts_amd import synthetic
     from oracle import ref_cpu
 
     torch.set_num_threads(threads)
     W = synthetic.make_weights_torch(arch)
     inp = synthetic.make_case(B=1, ref_frames=case["ref"], total_frames=case["total"], n_text=case["nt"])
-    t = {}
-    for ms in (1, 3):
-        t0 = time.perf_counter()
-        ref_cpu.cfm_sample(W, arch, inp["cond"], inp["text"], inp["duration"], lens=inp["lens"], steps=case["nfe"],
-                           cfg_strength=case["cfg"], sway_sampling_coef=case["sway"], seed=0, max_steps=ms)
-        t[ms] = time.perf_counter() - t0
-    step = (t[3] - t[1]) / 2
-    full = (t[1] - step) + case["nfe"] * step
+    t0 = time.perf_counter()
+    ref_cpu.cfm_sample(W, arch, inp["cond"], inp["text"], inp["duration"], lens=inp["lens"], steps=case["nfe"],
+                       cfg_strength=case["cfg"], sway_sampling_coef=case["sway"], seed=0)
+    full = time.perf_counter() - t0
     gen = case["total"] - case["ref"]
-    return {"value": gen / full, "unit": "mel-frames/s", "cores": torch.get_num_threads(), "kind": "port",
-            "sample": f"oracle/ref_cpu.py fp32, C2 call truncated to 1 and 3 Euler steps "
-                      f"({t[1]:.1f}s, {t[3]:.1f}s); full 16-step call extrapolated = {full:.1f}s",
-            "rtf": full / (gen * HOP / SR)}
+    return {"value": round(gen / full, 3), "unit": "mel-frames/s", "cores": torch.get_num_threads(), "kind": "port",
+            "sample": f"oracle/ref_cpu.py fp32, one full 16-step C2 call ({full:.1f}s, {gen} generated frames) "
+                      f"on {cpu_model()}, {torch.get_num_threads()} threads",
+            "rtf": round(full / (gen * HOP / SR), 4), "seconds": round(full, 2)}
 
 
 def class_flops(kc, arch, S, L):
@@ -109,23 +122,82 @@ def class_flops(kc, arch, S, L):
             "conv": 2.0 * S * L * d * (d // 16) * 31}.get(kc, 0.0)
 
 
+def class_bytes(kc, arch, S, L, esz=2):
+    """Algorithmic HBM bytes of one launch of an HBM-bound class: the pre-FFN norm reads the fp32
+    residual rows and writes the 16-bit GEMM operand."""
+    if kc == "norm":
+        return S * L * arch["dim"] * (4 + esz)
+    return 0.0
+
+
+PROBE_CLASSES = ("qkv", "attention", "out", "norm", "ffn1", "ffn2", "conv")
+PEAK_HBM_GBPS = 8000.0
+
+
+def class_entry(kc, avg_ms, n, arch, S, L, launches_per_call, ms_call):
+    fl = class_flops(kc, arch, S, L)
+    e = {"kernel": kc, "avg_launch_us": round(avg_ms * 1e3, 3), "sampled_launches": n,
+         "launches_per_call": launches_per_call,
+         "share_of_call": round(avg_ms * launches_per_call / ms_call, 4) if ms_call else None}
+    if fl:
+        ach = fl / (avg_ms * 1e-3) / 1e12
+        e.update(bound="mfma", achieved=round(ach, 2), peak=PEAK_BF16_TFLOPS, unit="TFLOP/s",
+                 frac=round(ach / PEAK_BF16_TFLOPS, 4), flops_per_launch=fl)
+    else:
+        by = class_bytes(kc, arch, S, L)
+        ach = by / (avg_ms * 1e-3) / 1e9 if by else 0.0
+        e.update(bound="hbm", achieved=round(ach, 1), peak=PEAK_HBM_GBPS, unit="GB/s",
+                 frac=round(ach / PEAK_HBM_GBPS, 4), bytes_per_launch=by)
+    traffic, src = pmc_traffic(kc)
+    e["traffic"] = traffic
+    e["traffic_source"] = src
+    if traffic and kc in ("qkv", "out", "ffn1", "ffn2", "attention"):
+        d, ff = arch["dim"], int(arch["dim"] * arch["ff_mult"])
+        kn = {"qkv": (d, 3 * d), "out": (d, d), "ffn1": (d, ff), "ffn2": (ff, d)}.get(kc)
+        if kn:  # operands + result at the operand width (fp32 residual read+write for RESID)
+            K, Nn = kn
+            alg = 2 * (S * L * K + Nn * K) + (8 if kc in ("out", "ffn2") else 2) * S * L * Nn
+        else:
+            alg = 4 * 2 * S * arch["heads"] * L * 64
+        e["algorithmic_bytes"] = alg
+        e["traffic_over_algorithmic"] = round(traffic / alg, 3)
+    return e
+
+
+def build_job(case, world):
+    """The whole job of this run: per-GPU utterances of the config x world (weak scaling), identical on
+    every rank (one seeded generator), as parallel.run_sharded utterance dicts."""
+    from f5_tts_amd import synthetic
+
+    B = case["B"]
+    refs = case["ref"] if isinstance(case["ref"], list) else [case["ref"]] * B
+    tots = case["total"] if isinstance(case["total"], list) else [case["total"]] * B
+    nts = case["nt"] if isinstance(case["nt"], list) else [case["nt"]] * B
+    refs, tots, nts = refs * world, tots * world, nts * world
+    inp = synthetic.make_case(B=B * world, ref_frames=refs, total_frames=tots, n_text=nts, seed=1234)
+    utts = []
+    for i in range(B * world):
+        utts.append(dict(cond=inp["cond"][i, : refs[i]], text=inp["text"][i, : nts[i]], ref=refs[i], total=tots[i]))
+    return utts
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--preset", default="F5TTS_v1_Base")
-    ap.add_argument("--compute", default="bf16")
+    ap.add_argument("--compute", default="bf16", choices=("bf16", "fp16", "fp32"))
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--probe", default="attention", help="kernel class timed live (in-kernel device wall-clock stamps) for the roofline")
+    ap.add_argument("--probe", default="auto",
+                    help="kernel class probed live over the timed region (in-kernel device wall-clock stamps); "
+                         "'auto' = the class with the largest share of the call in the probe pre-pass, 'none' = off")
     ap.add_argument("--config", default="c2", choices=("c2", "c3", "c4", "c5"),
                     help="workload (SURVEY §8d); c2 is the headline line")
     ap.add_argument("--no-vocos", action="store_true", help="skip the +Vocos decode timing (SURVEY §8f1)")
-    ap.add_argument("--probe-all", action="store_true",
-                    help="after the measurement, time every kernel class in its own loop (table on stderr)")
     args = ap.parse_args()
 
-    from f5_tts_amd import synthetic
+    from f5_tts_amd import parallel, synthetic
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -142,29 +214,60 @@ def main():
         case["preset"] = args.preset
     model, arch = build_model(case["preset"], args.compute, device)
     B = case["B"]
-    refs = case["ref"] if isinstance(case["ref"], list) else [case["ref"]] * B
-    tots = case["total"] if isinstance(case["total"], list) else [case["total"]] * B
-    inp = synthetic.make_case(B=B, ref_frames=refs, total_frames=tots, n_text=case["nt"], seed=1234 + rank)
-    cond, text = inp["cond"].to(device), inp["text"].to(device)
-    duration, lens = inp["duration"].to(device), inp["lens"].to(device)
-    gen_frames = sum(t - r for t, r in zip(tots, refs))
-    Nmax = max(tots)
-    gathered = torch.empty(world, gen_frames * 100, device=device)
+    utts = build_job(case, world)
+    for u in utts:  # inputs resident in HBM before anything is timed
+        u["cond"], u["text"] = u["cond"].to(device), u["text"].to(device)
+    batches = parallel.plan([u["total"] for u in utts], world, max_batch=B)[rank]
+    my = [i for b in batches for i in b]
+    gen_frames = sum(utts[i]["total"] - utts[i]["ref"] for i in my)
+    job_frames = sum(u["total"] - u["ref"] for u in utts)
+    Nmax = max(utts[i]["total"] for i in my)
+
+    def sample(cond, text, dur, lens):
+        out, _ = model.sample(cond=cond, text=text, duration=dur, lens=lens, steps=case["nfe"],
+                              cfg_strength=case["cfg"], sway_sampling_coef=case["sway"], seed=rank,
+                              keep_trajectory=False)
+        return out
 
     def step():
-        out, _ = model.sample(cond=cond, text=text, duration=duration, lens=lens, steps=case["nfe"],
-                              cfg_strength=case["cfg"], sway_sampling_coef=case["sway"], seed=rank)
-        mel = torch.cat([out[b, refs[b]:tots[b]].reshape(-1) for b in range(B)])
-        if world > 1:
-            dist.all_gather_into_tensor(gathered, mel)  # finished mels only
-        return mel
+        return parallel.run_sharded(utts, sample, rank=rank, world=world, device=device, batches=batches)
+
+    eng = model.transformer.get_engine(model.engine_compute(), device)
+    S = 2 * B if case["cfg"] >= 1e-5 else B
+    L = Nmax if arch["backbone"] == "DiT" else Nmax + 1
+    launches = {"norm": arch["depth"]}
+    for kc in ("qkv", "attention", "out", "ffn1", "ffn2"):
+        launches[kc] = arch["depth"]
+    launches["conv"] = 1
 
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
 
-    eng = model.transformer.get_engine(model.engine_compute(), device)
-    eng.probe(args.probe)
+    # ---- probe pre-pass: every kernel class timed by its in-kernel stamps, one call each
+    t0 = time.perf_counter()
+    step()
+    torch.cuda.synchronize()
+    ms_pre = (time.perf_counter() - t0) * 1e3
+    classes = {}
+    for kc in PROBE_CLASSES:
+        eng.probe(kc)
+        step()  # captures the probed step graph (the probe is part of the graph key)
+        step()
+        torch.cuda.synchronize()
+        n, ms = eng.probe_read()
+        eng.probe(None)
+        if n:
+            classes[kc] = class_entry(kc, ms / n, n, arch, S, L, launches[kc] * case["nfe"], ms_pre)
+    probe = args.probe
+    if probe == "auto":
+        probe = max(classes, key=lambda k: classes[k]["share_of_call"] or 0.0) if classes else "none"
+
+    # ---- timed region (the probed class stamped live; its graph captured before the region)
+    if probe != "none":
+        eng.probe(probe)
+        step()
+    torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -175,48 +278,24 @@ def main():
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    n_launch, probe_ms = eng.probe_read()
-    eng.probe(None)
+    roof = None
+    if probe != "none":
+        n_launch, probe_ms = eng.probe_read()
+        eng.probe(None)
+        if n_launch:
+            roof = class_entry(probe, probe_ms / n_launch, n_launch, arch, S, L, launches[probe] * case["nfe"],
+                               elapsed / args.steps * 1e3)
+            roof["timing"] = ("in-kernel s_memrealtime stamps: first workgroup start to last wave end of every "
+                              "launch of the class in every 4th ODE step inside the timed region")
     if world > 1:
         tt = torch.tensor([elapsed], device=device, dtype=torch.float64)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
 
-    frames = gen_frames * args.steps * world
+    frames = job_frames * args.steps
     value = frames / elapsed
     ms_per_step = elapsed / args.steps * 1e3
     rtf = elapsed / (frames * HOP / SR) * world  # wall / generated audio seconds, per GPU stream
-
-    S = 2 * B if case["cfg"] >= 1e-5 else B
-    H = arch["heads"]
-    L = Nmax if arch["backbone"] == "DiT" else Nmax + 1
-    roof = None
-    if n_launch:
-        avg_ms = probe_ms / n_launch
-        fl = class_flops(args.probe, arch, S, L)
-        ach = fl / (avg_ms * 1e-3) / 1e12 if fl else 0.0
-        traffic, tsrc = pmc_traffic(args.probe) if args.config == "c2" else (None, None)
-        roof = {"bound": "mfma", "kernel": args.probe, "achieved": round(ach, 2), "peak": PEAK_BF16_TFLOPS,
-                "unit": "TFLOP/s", "frac": round(ach / PEAK_BF16_TFLOPS, 4), "traffic": traffic,
-                "traffic_unit": "bytes/launch", "traffic_source": tsrc,
-                "avg_launch_ms": round(avg_ms, 5), "launches": n_launch, "flops_per_launch": fl,
-                "timing": "in-kernel s_memrealtime stamps: first workgroup start to last wave end of the probed "
-                          "kernel's launches in every 4th ODE step inside the timed region (all layers)"}
-
-    if args.probe_all and rank == 0:
-        import sys
-        for kc in ("qkv", "attention", "out", "norm", "ffn1", "ffn2", "conv"):
-            eng.probe(kc)
-            for _ in range(max(1, min(args.steps, 3))):
-                step()
-            torch.cuda.synchronize()
-            n, ms = eng.probe_read()
-            eng.probe(None)
-            if n:
-                avg = ms / n
-                fl = class_flops(kc, arch, S, L)
-                print(f"[probe] {kc:9s} sampled launches {n:5d}  avg {avg * 1e3:8.2f} us"
-                      + (f"  {fl / (avg * 1e-3) / 1e12:7.1f} TF/s" if fl else ""), file=sys.stderr, flush=True)
 
     # +Vocos ("report an optional +Vocos RTF once f1 exists"): the reference decodes each
     # generated mel after sampling (utils_infer.py:506-511, benchmark.py:430-435); timed separately
@@ -228,9 +307,8 @@ def main():
         voc = Vocos(compute="bf16")
         voc.load_state_dict(vocos_weights())
         voc.to(device)
-        out, _ = model.sample(cond=cond, text=text, duration=duration, lens=lens, steps=case["nfe"],
-                              cfg_strength=case["cfg"], sway_sampling_coef=case["sway"], seed=rank)
-        gens = [out[b, refs[b]:tots[b]].t().unsqueeze(0).float().contiguous() for b in range(B)]
+        mels = parallel.run_sharded(utts, sample, rank=rank, world=1, device=device, batches=batches)
+        gens = [mels[i].t().unsqueeze(0).float().contiguous() for i in my]
         for g in gens:
             voc.decode(g)
         torch.cuda.synchronize()
@@ -249,7 +327,8 @@ def main():
             dist.all_reduce(tt, op=dist.ReduceOp.MAX)
             vel = float(tt.item())
         v_ms = vel / args.steps * 1e3
-        vocos = {"ms_per_step": round(v_ms, 3), "rtf_with_vocos": round((ms_per_step + v_ms) / 1e3 / (gen_frames * HOP / SR), 5),
+        vocos = {"ms_per_step": round(v_ms, 3),
+                 "rtf_with_vocos": round((ms_per_step + v_ms) / 1e3 / (gen_frames * HOP / SR), 5),
                  "note": "Vocos mel-24khz decode of each generated mel (per utterance, as the reference), "
                          "synthetic weights; rtf_with_vocos = (CFM + Vocos wall) / generated audio seconds"}
 
@@ -257,18 +336,18 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu_baseline and args.config == "c2":
         cpu = cpu_baseline(case, arch, threads=min(16, os.cpu_count() or 1))
 
-    # whole-path algorithmic FLOPs: NFE * S * F(N) at the padded length
-    flops_call = case["nfe"] * S * seq_flops(arch, Nmax)
+    # whole-path algorithmic FLOPs: NFE * S * F(N) at the padded length, per rank
+    flops_call = case["nfe"] * S * seq_flops(arch, Nmax) * len(batches)
     # useful work of a mixed-length batch: each utterance at its own length
-    useful_call = case["nfe"] * (S // B) * sum(seq_flops(arch, t) for t in tots)
+    useful_call = case["nfe"] * (S // B) * sum(seq_flops(arch, utts[i]["total"]) for i in my)
     if rank == 0:
         workloads = {
             "c2": "C2: F5TTS_v1_Base CFM.sample, NFE 16 EPSS + sway -1, CFG 2.0, 1 utterance per GPU, "
                   "938 prompt + 938 generated frames (1876), 300 tokens",
             "c3": "C3: F5TTS_v1_Base CFM.sample, NFE 32 linspace + sway -1, CFG 2.0, 32 utterances per GPU, "
                   "564..1876 frames (half prompt), padded to 1876, batch-mask path",
-            "c4": "C4 (per rank): F5TTS_v1_Base CFM.sample, NFE 16 EPSS + sway -1, CFG 2.0, 32 utterances per GPU "
-                  "(256 over 8 GPUs), 938 prompt + 938 generated frames each, 300 tokens, batch path",
+            "c4": "C4 (32 per GPU): F5TTS_v1_Base CFM.sample, NFE 16 EPSS + sway -1, CFG 2.0, 32 x world utterances "
+                  "(256 over 8 GPUs) LPT-sharded, 938 prompt + 938 generated frames each, 300 tokens, batch path",
             "c5": "C5: E2TTS_Base (UNetT) CFM.sample, NFE 16 EPSS + sway -1, CFG 2.0, 8 utterances per GPU, "
                   "938 prompt + 938 generated frames, 300 tokens",
         }
@@ -286,11 +365,12 @@ def main():
             "dtype": args.compute,
             "data": f"synthetic (hash-PRNG weights of {case['preset']}, N(-4,2) cond mel, uniform text ids)",
             "config": {"workload": workloads[args.config], "batch_per_gpu": B, "frames": Nmax,
-                       "gen_frames": gen_frames, "nfe": case["nfe"], "parallelism": f"dp{world}"},
+                       "gen_frames_per_gpu": gen_frames, "nfe": case["nfe"], "parallelism": f"dp{world}"},
             "rtf": round(rtf, 5),
             "path_tflops": round(flops_call * args.steps * world / elapsed / 1e12, 2),
             "path_tflops_useful": round(useful_call * args.steps * world / elapsed / 1e12, 2),
             "roofline": roof,
+            "roofline_classes": classes,
             "vocos": vocos,
             "cpu_baseline": cpu,
         }

@@ -10,6 +10,9 @@
 typedef __bf16 bf16;
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef _Float16 f16;
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
 typedef short s16x4 __attribute__((ext_vector_type(4)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
@@ -25,8 +28,36 @@ F5H_DEV float bf2f(bf16 x) { return (float)x; }
 template <typename T> F5H_DEV T from_f32(float x);
 template <> F5H_DEV float from_f32<float>(float x) { return x; }
 template <> F5H_DEV bf16 from_f32<bf16>(float x) { return f2bf(x); }
+template <> F5H_DEV f16 from_f32<f16>(float x) { return (f16)x; }  // RNE (v_cvt_f16_f32)
 F5H_DEV float to_f32(float x) { return x; }
 F5H_DEV float to_f32(bf16 x) { return bf2f(x); }
+F5H_DEV float to_f32(f16 x) { return (float)x; }
+
+// 16-bit operand types (bf16 perf mode, fp16 mode = the reference's default GPU dtype,
+// utils_infer.py:190-199): vector types and the two MFMA shapes (same cycles for both dtypes,
+// MI355X_MICROARCH.md "Matrix cores").
+template <typename T> struct Op16;
+template <> struct Op16<bf16> {
+  typedef bf16x8 v8;
+  typedef bf16x4 v4;
+  static F5H_DEV f32x4 mma16(const v8& a, const v8& b, f32x4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+  }
+  static F5H_DEV f32x16 mma32(const v8& a, const v8& b, f32x16 c) {
+    return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+  }
+};
+template <> struct Op16<f16> {
+  typedef f16x8 v8;
+  typedef f16x4 v4;
+  static F5H_DEV f32x4 mma16(const v8& a, const v8& b, f32x4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
+  }
+  static F5H_DEV f32x16 mma32(const v8& a, const v8& b, f32x16 c) {
+    return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
+  }
+};
+template <typename T> __host__ __device__ constexpr bool is16() { return sizeof(T) == 2; }
 
 // ---------------------------------------------------------------- activations
 F5H_DEV float gelu_tanh(float x) {  // nn.GELU(approximate="tanh"), modules.py:358
@@ -142,6 +173,12 @@ template <> struct Slab<bf16> {
     return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
   }
 };
+template <> struct Slab<f16> {
+  typedef f16x8 frag;
+  static F5H_DEV f32x4 mma(const frag& a, const frag& b, f32x4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
+  }
+};
 template <> struct Slab<float> {
   typedef f32x4 frag;
   static F5H_DEV f32x4 mma(const frag& a, const frag& b, f32x4 c) {
@@ -166,6 +203,20 @@ template <> struct Load16<float, float> {
     return ok ? *reinterpret_cast<const uint4*>(p) : make_uint4(0, 0, 0, 0);
   }
 };
+template <> struct Load16<f16, f16> {
+  static F5H_DEV uint4 ld(const f16* p, bool ok) {
+    return ok ? *reinterpret_cast<const uint4*>(p) : make_uint4(0, 0, 0, 0);
+  }
+};
+template <> struct Load16<f16, float> {
+  static F5H_DEV uint4 ld(const float* p, bool ok) {
+    if (!ok) return make_uint4(0, 0, 0, 0);
+    float4 a = *reinterpret_cast<const float4*>(p);
+    float4 b = *reinterpret_cast<const float4*>(p + 4);
+    f16x8 v = {(f16)a.x, (f16)a.y, (f16)a.z, (f16)a.w, (f16)b.x, (f16)b.y, (f16)b.z, (f16)b.w};
+    return __builtin_bit_cast(uint4, v);
+  }
+};
 template <> struct Load16<bf16, float> {
   static F5H_DEV uint4 ld(const float* p, bool ok) {
     if (!ok) return make_uint4(0, 0, 0, 0);
@@ -188,3 +239,23 @@ F5H_DEV void static_for(F&& f) {
     static_for<B + 1, E>(f);
   }
 }
+
+// Launch a templated kernel body for the compute mode's operand type: T = float (F5H_C_FP32),
+// bf16 (F5H_C_BF16) or f16 (F5H_C_FP16). Usage: F5H_OP_DISPATCH(compute, T, { launch<T>(...); });
+#define F5H_OP_DISPATCH(compute, T, ...)  \
+  do {                                     \
+    switch (compute) {                     \
+      case f5h::F5H_C_BF16: {              \
+        typedef bf16 T;                    \
+        __VA_ARGS__;                       \
+      } break;                             \
+      case f5h::F5H_C_FP16: {              \
+        typedef f16 T;                     \
+        __VA_ARGS__;                       \
+      } break;                             \
+      default: {                           \
+        typedef float T;                   \
+        __VA_ARGS__;                       \
+      }                                    \
+    }                                      \
+  } while (0)

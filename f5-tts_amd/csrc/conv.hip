@@ -136,13 +136,14 @@ __global__ __launch_bounds__(128 * NWM, 1) void conv_kernel(ConvArgs a) {
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
       float x = keep ? Cs[row * CP + c8 + e] + a.bias[oc + e] : 0.f;
-      v[e] = std::is_same<TC, bf16>::value ? mish_fast(x) : mish(x);
+      v[e] = is16<TC>() ? mish_fast(x) : mish(x);
     }
     if (a.mode == 0) {
       TC* y = reinterpret_cast<TC*>(a.y) + ((int64_t)s * L + pos) * d + oc;
-      if constexpr (std::is_same<TC, bf16>::value) {
-        bf16x8 o = {f2bf(v[0]), f2bf(v[1]), f2bf(v[2]), f2bf(v[3]), f2bf(v[4]), f2bf(v[5]), f2bf(v[6]), f2bf(v[7])};
-        *reinterpret_cast<bf16x8*>(y) = o;
+      if constexpr (is16<TC>()) {
+        typename Op16<TC>::v8 o = {from_f32<TC>(v[0]), from_f32<TC>(v[1]), from_f32<TC>(v[2]), from_f32<TC>(v[3]),
+                                   from_f32<TC>(v[4]), from_f32<TC>(v[5]), from_f32<TC>(v[6]), from_f32<TC>(v[7])};
+        *reinterpret_cast<typename Op16<TC>::v8*>(y) = o;
       } else {
 #pragma unroll
         for (int e = 0; e < 8; ++e) y[e] = from_f32<TC>(v[e]);
@@ -160,12 +161,19 @@ __global__ __launch_bounds__(128 * NWM, 1) void conv_kernel(ConvArgs a) {
 hipError_t conv_pos(int compute, const ConvArgs& a, hipStream_t st) {
   // groups = 16; d/16 channels per group, padded to the 64-channel tile (d % 128 == 0)
   if (a.d % 128 != 0 || a.d > 1024) return hipErrorInvalidValue;
-  if (compute) {
+  if (compute == F5H_C_BF16 || compute == F5H_C_FP16) {
     dim3 grid((a.L + 127) / 128, 16, a.S);
-    if (a.x_f32)
-      hipLaunchKernelGGL((conv_kernel<bf16, float, 4>), grid, dim3(512), 0, st, a);
-    else
-      hipLaunchKernelGGL((conv_kernel<bf16, bf16, 4>), grid, dim3(512), 0, st, a);
+    if (compute == F5H_C_BF16) {
+      if (a.x_f32)
+        hipLaunchKernelGGL((conv_kernel<bf16, float, 4>), grid, dim3(512), 0, st, a);
+      else
+        hipLaunchKernelGGL((conv_kernel<bf16, bf16, 4>), grid, dim3(512), 0, st, a);
+    } else {
+      if (a.x_f32)
+        hipLaunchKernelGGL((conv_kernel<f16, float, 4>), grid, dim3(512), 0, st, a);
+      else
+        hipLaunchKernelGGL((conv_kernel<f16, f16, 4>), grid, dim3(512), 0, st, a);
+    }
   } else {
     dim3 grid((a.L + 63) / 64, 16, a.S);
     hipLaunchKernelGGL((conv_kernel<float, float, 2>), grid, dim3(256), 0, st, a);

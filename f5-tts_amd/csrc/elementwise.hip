@@ -15,11 +15,15 @@ template <> F5H_DEV void store4<bf16>(bf16* p, float a, float b, float c, float 
   bf16x4 v = {f2bf(a), f2bf(b), f2bf(c), f2bf(d)};
   *reinterpret_cast<bf16x4*>(p) = v;
 }
+template <> F5H_DEV void store4<f16>(f16* p, float a, float b, float c, float d) {
+  f16x4 v = {(f16)a, (f16)b, (f16)c, (f16)d};
+  *reinterpret_cast<f16x4*>(p) = v;
+}
 
 // ---------------------------------------------------------------- time embedding
 // SinusPositionEmbedding(256), scale 1000 (modules.py:157-169): [sin | cos](1000 t e^{-i ln1e4/127})
-struct TVals {
-  float t[512];
+struct TVals {  // up to 512 NFE steps: 513 grid points (kernel-argument payload, 2 KB)
+  float t[513];
 };
 __global__ void time_sinus_kernel(TVals tv, int n, float* out) {
   int i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -55,7 +59,7 @@ hipError_t ptr_upload(float* p, float** slot, hipStream_t st) {
   return hipGetLastError();
 }
 hipError_t grid_upload(const float* t_host, int n, float* out, hipStream_t st) {
-  if (n <= 0 || n > 512) return hipErrorInvalidValue;
+  if (n <= 0 || n > 513) return hipErrorInvalidValue;
   TVals tv{};
   for (int i = 0; i < n; ++i) tv.t[i] = t_host[i];
   hipLaunchKernelGGL(grid_upload_kernel, dim3(nblk(n, 256)), dim3(256), 0, st, tv, n, out);
@@ -115,10 +119,7 @@ __global__ void silu_kernel(const float* x, TO* y, int64_t n) {
   if (i < n) y[i] = from_f32<TO>(silu(x[i]));
 }
 hipError_t silu_to_op(int compute, const float* x, void* y, int64_t n, hipStream_t st) {
-  if (compute)
-    hipLaunchKernelGGL(silu_kernel<bf16>, dim3(nblk(n, 256)), dim3(256), 0, st, x, (bf16*)y, n);
-  else
-    hipLaunchKernelGGL(silu_kernel<float>, dim3(nblk(n, 256)), dim3(256), 0, st, x, (float*)y, n);
+  F5H_OP_DISPATCH(compute, T, hipLaunchKernelGGL(silu_kernel<T>, dim3(nblk(n, 256)), dim3(256), 0, st, x, (T*)y, n););
   return hipGetLastError();
 }
 
@@ -169,10 +170,7 @@ __global__ void ln_mod_kernel(const float* h, int M, int d, const float* shift, 
 hipError_t ln_modulate(int compute, const float* h, int M, int d, const float* shift, const float* scale, void* out,
                        hipStream_t st) {
   if (d % 4 || d > 4 * 64 * MAXV) return hipErrorInvalidValue;
-  if (compute)
-    hipLaunchKernelGGL(ln_mod_kernel<bf16>, dim3(nblk(M, 4)), dim3(256), 0, st, h, M, d, shift, scale, (bf16*)out);
-  else
-    hipLaunchKernelGGL(ln_mod_kernel<float>, dim3(nblk(M, 4)), dim3(256), 0, st, h, M, d, shift, scale, (float*)out);
+  F5H_OP_DISPATCH(compute, T, hipLaunchKernelGGL(ln_mod_kernel<T>, dim3(nblk(M, 4)), dim3(256), 0, st, h, M, d, shift, scale, (T*)out););
   return hipGetLastError();
 }
 
@@ -206,10 +204,7 @@ __global__ void rms_kernel(const float* h, int M, int d, const float* g, TO* out
 }
 hipError_t rms_norm_g(int compute, const float* h, int M, int d, const float* g, void* out, hipStream_t st) {
   if (d % 4 || d > 4 * 64 * MAXV) return hipErrorInvalidValue;
-  if (compute)
-    hipLaunchKernelGGL(rms_kernel<bf16>, dim3(nblk(M, 4)), dim3(256), 0, st, h, M, d, g, (bf16*)out);
-  else
-    hipLaunchKernelGGL(rms_kernel<float>, dim3(nblk(M, 4)), dim3(256), 0, st, h, M, d, g, (float*)out);
+  F5H_OP_DISPATCH(compute, T, hipLaunchKernelGGL(rms_kernel<T>, dim3(nblk(M, 4)), dim3(256), 0, st, h, M, d, g, (T*)out););
   return hipGetLastError();
 }
 
@@ -303,12 +298,7 @@ __global__ void dwconv_ln_kernel(const float* x, int S, int L, int C, const floa
 hipError_t dwconv_ln(int compute, const float* x, int S, int L, int C, const float* dw_w, const float* dw_b,
                      const float* ln_w, const float* ln_b, void* out, hipStream_t st) {
   if (C > 1024) return hipErrorInvalidValue;
-  if (compute)
-    hipLaunchKernelGGL(dwconv_ln_kernel<bf16>, dim3(nblk(S * L, 4)), dim3(256), 0, st, x, S, L, C, dw_w, dw_b, ln_w,
-                       ln_b, (bf16*)out);
-  else
-    hipLaunchKernelGGL(dwconv_ln_kernel<float>, dim3(nblk(S * L, 4)), dim3(256), 0, st, x, S, L, C, dw_w, dw_b,
-                       ln_w, ln_b, (float*)out);
+  F5H_OP_DISPATCH(compute, T, hipLaunchKernelGGL(dwconv_ln_kernel<T>, dim3(nblk(S * L, 4)), dim3(256), 0, st, x, S, L, C, dw_w, dw_b, ln_w, ln_b, (T*)out););
   return hipGetLastError();
 }
 
@@ -370,20 +360,17 @@ hipError_t grn(int compute, const float* x, int S, int L, int C, const float* ga
   hipLaunchKernelGGL(grn_norm_kernel, dim3(S), dim3(1024), 0, st, scratch, nz, S, C, nx);
   scratch = nx;
   const int64_t total = (int64_t)S * L * C;
-  if (compute)
-    hipLaunchKernelGGL(grn_apply_kernel<bf16>, dim3(nblk(total, 256)), dim3(256), 0, st, x, L, C, scratch, gamma,
-                       beta, (bf16*)out, total);
-  else
-    hipLaunchKernelGGL(grn_apply_kernel<float>, dim3(nblk(total, 256)), dim3(256), 0, st, x, L, C, scratch, gamma,
-                       beta, (float*)out, total);
+  F5H_OP_DISPATCH(compute, T, hipLaunchKernelGGL(grn_apply_kernel<T>, dim3(nblk(total, 256)), dim3(256), 0, st, x, L, C, scratch, gamma, beta, (T*)out, total););
   return hipGetLastError();
 }
 
 // ---------------------------------------------------------------- input-projection operands
-// A_ct row (s, n) = [step_cond (or 0 for the uncond branch, dit.py:155-156) pad->128 | text_e pad->tdp]
+// A_ct row (s, n) = [step_cond (or 0 for the uncond branch, dit.py:155-156) pad->128 | text_e pad->tdp].
+// Rows s < B are the conditional branch; a single-branch forward (cfg_infer=False, dit.py:347-350)
+// may drop the audio cond (InputEmbedding drop_audio_cond) and/or use the dropped-text embedding.
 template <typename TO>
 __global__ void build_ct_kernel(const float* cond, const uint8_t* cmask, const float* tc, const float* tu, int B,
-                                int N, int td, int tdp, int S, TO* out) {
+                                int N, int td, int tdp, int S, int drop_audio, int drop_text, TO* out) {
   const int64_t K = 128 + tdp;
   int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= (int64_t)S * N * K) return;
@@ -393,23 +380,19 @@ __global__ void build_ct_kernel(const float* cond, const uint8_t* cmask, const f
   const int b = s % B;
   float v = 0.f;
   if (col < 128) {
-    if (col < 100 && s < B && cmask[(int64_t)b * N + n]) v = cond[((int64_t)b * N + n) * 100 + col];
+    if (col < 100 && s < B && !drop_audio && cmask[(int64_t)b * N + n]) v = cond[((int64_t)b * N + n) * 100 + col];
   } else if (col - 128 < td) {
-    const float* t = s < B ? tc : tu;
+    const float* t = (s < B && !drop_text) ? tc : tu;
     v = t[((int64_t)b * N + n) * td + (col - 128)];
   }
   out[i] = from_f32<TO>(v);
 }
 hipError_t build_ct(int compute, const float* cond, const uint8_t* cond_mask, const float* text_c,
-                    const float* text_u, int B, int N, int td, int S, void* out, hipStream_t st) {
+                    const float* text_u, int B, int N, int td, int S, int drop_audio, int drop_text, void* out,
+                    hipStream_t st) {
   const int tdp = (td + 63) / 64 * 64;
   const int64_t total = (int64_t)S * N * (128 + tdp);
-  if (compute)
-    hipLaunchKernelGGL(build_ct_kernel<bf16>, dim3(nblk(total, 256)), dim3(256), 0, st, cond, cond_mask, text_c,
-                       text_u, B, N, td, tdp, S, (bf16*)out);
-  else
-    hipLaunchKernelGGL(build_ct_kernel<float>, dim3(nblk(total, 256)), dim3(256), 0, st, cond, cond_mask, text_c,
-                       text_u, B, N, td, tdp, S, (float*)out);
+  F5H_OP_DISPATCH(compute, T, hipLaunchKernelGGL(build_ct_kernel<T>, dim3(nblk(total, 256)), dim3(256), 0, st, cond, cond_mask, text_c, text_u, B, N, td, tdp, S, drop_audio, drop_text, (T*)out););
   return hipGetLastError();
 }
 
@@ -423,10 +406,7 @@ __global__ void pack_y_kernel(const float* y, int rows, int mel, TO* yp) {
 }
 hipError_t pack_y(int compute, const float* y, int rows, int mel, void* ypad, hipStream_t st) {
   const int64_t total = (int64_t)rows * 128;
-  if (compute)
-    hipLaunchKernelGGL(pack_y_kernel<bf16>, dim3(nblk(total, 256)), dim3(256), 0, st, y, rows, mel, (bf16*)ypad);
-  else
-    hipLaunchKernelGGL(pack_y_kernel<float>, dim3(nblk(total, 256)), dim3(256), 0, st, y, rows, mel, (float*)ypad);
+  F5H_OP_DISPATCH(compute, T, hipLaunchKernelGGL(pack_y_kernel<T>, dim3(nblk(total, 256)), dim3(256), 0, st, y, rows, mel, (T*)ypad););
   return hipGetLastError();
 }
 
@@ -461,10 +441,7 @@ __global__ void cfg_euler_kernel(EulerArgs a, TO* ypad) {
 }
 hipError_t cfg_euler(const EulerArgs& a, hipStream_t st) {
   const int64_t total = (int64_t)a.B * a.N * a.mel;
-  if (a.compute)
-    hipLaunchKernelGGL(cfg_euler_kernel<bf16>, dim3(nblk(total, 256)), dim3(256), 0, st, a, (bf16*)a.ypad);
-  else
-    hipLaunchKernelGGL(cfg_euler_kernel<float>, dim3(nblk(total, 256)), dim3(256), 0, st, a, (float*)a.ypad);
+  F5H_OP_DISPATCH(a.compute, T, hipLaunchKernelGGL(cfg_euler_kernel<T>, dim3(nblk(total, 256)), dim3(256), 0, st, a, (T*)a.ypad););
   return hipGetLastError();
 }
 
@@ -552,17 +529,11 @@ __global__ void cvt_back_kernel(const TI* x, int64_t n, float* y) {
   if (i < n) y[i] = to_f32(x[i]);
 }
 hipError_t f32_to_op(int compute, const float* x, int64_t n, void* out, hipStream_t st) {
-  if (compute)
-    hipLaunchKernelGGL(cvt_kernel<bf16>, dim3(nblk(n, 256)), dim3(256), 0, st, x, n, (bf16*)out);
-  else
-    hipLaunchKernelGGL(cvt_kernel<float>, dim3(nblk(n, 256)), dim3(256), 0, st, x, n, (float*)out);
+  F5H_OP_DISPATCH(compute, T, hipLaunchKernelGGL(cvt_kernel<T>, dim3(nblk(n, 256)), dim3(256), 0, st, x, n, (T*)out););
   return hipGetLastError();
 }
 hipError_t op_to_f32(int compute, const void* x, int64_t n, float* out, hipStream_t st) {
-  if (compute)
-    hipLaunchKernelGGL(cvt_back_kernel<bf16>, dim3(nblk(n, 256)), dim3(256), 0, st, (const bf16*)x, n, out);
-  else
-    hipLaunchKernelGGL(cvt_back_kernel<float>, dim3(nblk(n, 256)), dim3(256), 0, st, (const float*)x, n, out);
+  F5H_OP_DISPATCH(compute, T, hipLaunchKernelGGL(cvt_back_kernel<T>, dim3(nblk(n, 256)), dim3(256), 0, st, (const T*)x, n, out););
   return hipGetLastError();
 }
 

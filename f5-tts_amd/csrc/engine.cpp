@@ -18,6 +18,7 @@
 #include <cstring>
 #include <algorithm>
 #include <atomic>
+#include <memory>
 #include <mutex>
 #include <string>
 #include <unordered_map>
@@ -54,6 +55,13 @@ static uint16_t f2bf_host(float f) {
   return (uint16_t)(u >> 16);
 }
 
+static uint16_t f2h_host(float f) {  // round-to-nearest-even fp32 -> fp16 (clang _Float16 on the host)
+  _Float16 h = (_Float16)f;
+  uint16_t u;
+  std::memcpy(&u, &h, 2);
+  return u;
+}
+
 struct Lin {
   void* w = nullptr;      // [Npad][K] operand dtype
   float* b = nullptr;     // [Npad] fp32 (may be null)
@@ -73,7 +81,7 @@ struct Layer {
 struct f5h_engine {
   f5h_arch a{};
   int dev = 0;
-  int bf = 0;          // compute == BF16
+  int bf = 0;          // compute mode (f5h_compute == ComputeMode): 0 fp32, 1 bf16, 2 fp16 operands
   size_t esz = 4;      // operand element size
   int tdp = 0;         // text_dim padded to 64
   std::vector<void*> allocs;
@@ -87,7 +95,7 @@ struct f5h_engine {
   float* norm_out_g = nullptr;
   // hipGraph cache of one NFE step (keyed by the call's buffers and shape)
   std::mutex gm;
-  std::vector<struct GraphEntry*> graphs;
+  std::vector<std::shared_ptr<struct GraphEntry>> graphs;
   hipStream_t cap = nullptr;  // private capture stream (the caller's may be the null stream)
   int graph_mode = 1;
   uint64_t use_ctr = 0;
@@ -123,16 +131,20 @@ struct GraphKey {
            use_cfg == o.use_cfg && batch_mask == o.batch_mask && probe == o.probe && cfg_bits == o.cfg_bits;
   }
 };
+// Shared by the cache and by every call replaying it: an entry evicted while another thread is
+// still in its launch loop is destroyed by the last holder, after the device has drained (an
+// already-submitted replay may still be executing).
 struct GraphEntry {
   GraphKey key{};
   hipGraphExec_t exec = nullptr;
   uint64_t stamp = 0;
+  ~GraphEntry() {
+    if (exec) {
+      (void)hipDeviceSynchronize();
+      (void)hipGraphExecDestroy(exec);
+    }
+  }
 };
-static void graph_entry_free(GraphEntry* g) {
-  if (!g) return;
-  if (g->exec) (void)hipGraphExecDestroy(g->exec);
-  delete g;
-}
 
 // ---------------------------------------------------------------- weight packing
 struct WMap {
@@ -165,7 +177,10 @@ static int upload(f5h_engine* e, const std::vector<T>& h, T** out) {
 static int upload_op(f5h_engine* e, const std::vector<float>& h, void** out) {
   if (e->bf) {
     std::vector<uint16_t> b(h.size());
-    for (size_t i = 0; i < h.size(); ++i) b[i] = f2bf_host(h[i]);
+    if (e->bf == F5H_FP16)
+      for (size_t i = 0; i < h.size(); ++i) b[i] = f2h_host(h[i]);
+    else
+      for (size_t i = 0; i < h.size(); ++i) b[i] = f2bf_host(h[i]);
     uint16_t* p;
     int rc = upload(e, b, &p);
     *out = p;
@@ -478,6 +493,7 @@ struct Ctx {
   hipStream_t st;
   Bufs b;
   int B, N, nt, S, L, nfe, use_cfg, batch_mask;
+  int drop_audio, drop_text;  // single-branch forward only (f5h_forward with cfg_infer = 0)
   int site;  // probe launch-site counter, reset at the start of every step's enqueue
 };
 
@@ -561,7 +577,8 @@ static int prologue(Ctx& c, const float* t_host, int nt_vals, const float* cond,
     }
   }
   // ---- hoisted input projection: P = [step_cond | text] . W_ct^T + b
-  KCK(build_ct(bf, cond, cond_mask, b.te, b.te + (size_t)c.B * c.N * td, c.B, c.N, td, c.S, b.act, st));
+  KCK(build_ct(bf, cond, cond_mask, b.te, b.te + (size_t)c.B * c.N * td, c.B, c.N, td, c.S, c.drop_audio,
+               c.drop_text, b.act, st));
   GemmArgs g = gargs(b.act, 128 + e->tdp, e->in_ct, c.S * c.N, b.P, d);
   KCK(gemm(bf, EPI_STORE, g, st));
   return 0;
@@ -723,7 +740,8 @@ static int check_arch(const f5h_arch* a) {
   if (a->text_dim <= 0 || a->text_dim % 4 || a->text_dim > 512) return fail(F5H_EINVAL, "text_dim must be <= 512, % 4");
   if (a->depth <= 0 || (a->backbone == F5H_UNETT && a->depth % 2)) return fail(F5H_EINVAL, "bad depth");
   if (a->backbone == F5H_UNETT && a->conv_layers != 0) return fail(F5H_EINVAL, "UNetT with conv_layers unsupported");
-  if (a->compute != F5H_FP32 && a->compute != F5H_BF16) return fail(F5H_EINVAL, "compute must be FP32 or BF16");
+  if (a->compute != F5H_FP32 && a->compute != F5H_BF16 && a->compute != F5H_FP16)
+    return fail(F5H_EINVAL, "compute must be FP32, BF16 or FP16");
   return 0;
 }
 
@@ -742,7 +760,7 @@ int f5h_engine_create(const f5h_arch* arch, const f5h_weight* weights, int32_t n
   f5h_engine* e = new f5h_engine();
   e->a = *arch;
   e->dev = device;
-  e->bf = arch->compute == F5H_BF16;
+  e->bf = arch->compute;
   e->esz = e->bf ? 2 : 4;
   e->tdp = (arch->text_dim + 63) / 64 * 64;
   if (const char* gv = getenv("F5H_GRAPH")) e->graph_mode = atoi(gv) ? 1 : 0;
@@ -773,7 +791,7 @@ int f5h_engine_create(const f5h_arch* arch, const f5h_weight* weights, int32_t n
 
 void f5h_engine_destroy(f5h_engine* e) {
   if (!e) return;
-  for (GraphEntry* g : e->graphs) graph_entry_free(g);
+  e->graphs.clear();
   if (e->cap) (void)hipStreamDestroy(e->cap);
   for (void* p : e->allocs) (void)hipFree(p);
   delete e;
@@ -885,29 +903,24 @@ static int run_steps(Ctx& c, const f5h_sample_args* a, const void* ws) {
   key.probe = e->probe_class;
   key.kernel_epoch = g_kernel_epoch.load();
   std::memcpy(&key.cfg_bits, &a->cfg_strength, 4);
-  hipGraphExec_t exec = nullptr;
+  std::shared_ptr<GraphEntry> hold;  // keeps the replayed graph alive through the launch loop
   {
     std::lock_guard<std::mutex> g(e->gm);
-    GraphEntry* hit = nullptr;
-    for (GraphEntry* x : e->graphs)
-      if (x->key == key) hit = x;
-    if (!hit) {
+    for (const auto& x : e->graphs)
+      if (x->key == key) hold = x;
+    if (!hold) {
       if (!e->cap) HIPCK(hipStreamCreateWithFlags(&e->cap, hipStreamNonBlocking));
-      GraphEntry* ne = new GraphEntry();
+      auto ne = std::make_shared<GraphEntry>();
       ne->key = key;
       Ctx cc = c;
       cc.st = e->cap;
       hipError_t be = hipStreamBeginCapture(e->cap, hipStreamCaptureModeThreadLocal);
-      if (be != hipSuccess) {
-        graph_entry_free(ne);
-        return fail(F5H_EHIP, std::string("hipStreamBeginCapture: ") + hipGetErrorString(be));
-      }
+      if (be != hipSuccess) return fail(F5H_EHIP, std::string("hipStreamBeginCapture: ") + hipGetErrorString(be));
       const int rc = enqueue_step(cc, a);
       hipGraph_t graph = nullptr;
       const hipError_t ce = hipStreamEndCapture(e->cap, &graph);
       if (rc || ce != hipSuccess) {
         if (graph) (void)hipGraphDestroy(graph);
-        graph_entry_free(ne);
         if (rc) return rc;
         return fail(F5H_EHIP, std::string("hipStreamEndCapture: ") + hipGetErrorString(ce));
       }
@@ -915,26 +928,22 @@ static int run_steps(Ctx& c, const f5h_sample_args* a, const void* ws) {
       (void)hipGraphDestroy(graph);
       if (ie != hipSuccess) {
         ne->exec = nullptr;
-        graph_entry_free(ne);
         return fail(F5H_EHIP, std::string("hipGraphInstantiate: ") + hipGetErrorString(ie));
       }
       if (e->graphs.size() >= 8) {  // evict the least recently used step graph
-        (void)hipDeviceSynchronize();  // it may still be in flight on another stream
         size_t lru = 0;
         for (size_t i = 1; i < e->graphs.size(); ++i)
           if (e->graphs[i]->stamp < e->graphs[lru]->stamp) lru = i;
-        graph_entry_free(e->graphs[lru]);
-        e->graphs.erase(e->graphs.begin() + lru);
+        e->graphs.erase(e->graphs.begin() + lru);  // destroyed now, or by its last replaying caller
       }
       e->graphs.push_back(ne);
       e->n_captures++;
-      hit = ne;
+      hold = ne;
     }
-    hit->stamp = ++e->use_ctr;
-    exec = hit->exec;
+    hold->stamp = ++e->use_ctr;
     e->n_replays += c.nfe;
   }
-  for (int k = 0; k < c.nfe; ++k) HIPCK(hipGraphLaunch(exec, c.st));
+  for (int k = 0; k < c.nfe; ++k) HIPCK(hipGraphLaunch(hold->exec, c.st));
   return 0;
 }
 
@@ -951,11 +960,14 @@ int f5h_forward(f5h_engine* e, void* stream, const f5h_forward_args* a, void* wo
   c.N = a->N;
   c.nt = a->nt;
   c.nfe = 1;
-  c.use_cfg = 1;
-  c.S = 2 * c.B;
+  c.use_cfg = a->cfg_infer ? 1 : 0;
+  c.S = c.use_cfg ? 2 * c.B : c.B;
+  c.drop_audio = (!c.use_cfg && a->drop_audio_cond) ? 1 : 0;
+  c.drop_text = (!c.use_cfg && a->drop_text) ? 1 : 0;
   c.L = e->a.backbone == F5H_DIT ? c.N : c.N + 1;
   c.batch_mask = a->use_batch_mask ? 1 : 0;
-  RC(check_ws(e, c.B, c.N, 1, 1, workspace, workspace_bytes, c));
+  if (e->a.backbone == F5H_DIT && a->N > 8192) return fail(F5H_EINVAL, "N exceeds the text position table (8192)");
+  RC(check_ws(e, c.B, c.N, 1, c.use_cfg, workspace, workspace_bytes, c));
   float tg[2] = {a->t, a->t};
   RC(prologue(c, tg, 1, a->cond, a->cond_mask, a->text, a->duration));
   HIPCK(pack_y(e->bf, a->x, c.B * c.N, e->a.mel_dim, c.b.ypad, c.st));
@@ -1032,6 +1044,7 @@ int f5h_graph_stats(f5h_engine* e, int64_t* captures, int64_t* replays, int32_t*
 int f5h_op_linear(void* stream, int32_t compute, int32_t M, int32_t N, int32_t K, const float* A, const float* W,
                   const float* bias, float* C, void* workspace, size_t workspace_bytes) {
   if (M <= 0 || N <= 0 || K <= 0 || K % 64) return fail(F5H_EINVAL, "op_linear needs K % 64 == 0");
+  if (compute < F5H_FP32 || compute > F5H_FP16) return fail(F5H_EINVAL, "bad compute mode");
   const int Npad = (N + 127) / 128 * 128;
   const size_t es = compute ? 2 : 4;
   const size_t need = (size_t)Npad * K * es;
@@ -1062,21 +1075,9 @@ int f5h_op_linear(void* stream, int32_t compute, int32_t M, int32_t N, int32_t K
 }
 
 int f5h_gemm_force_config(int32_t cfg) {
-  if (cfg < -1 || (cfg > 7 && cfg < 10) || cfg > 17) return fail(F5H_EINVAL, "gemm config must be -1..7 or 10..17");
+  if (cfg != -1 && cfg != 0 && cfg != 1 && cfg != 5 && cfg != 11)
+    return fail(F5H_EINVAL, "gemm config must be -1, 0, 1, 5 or 11");
   gemm_force_config(cfg);
-  g_kernel_epoch.fetch_add(1);
-  return 0;
-}
-
-int f5h_debug_attn_stamps(uint64_t* out, int32_t n) {
-  HIPCK(attn_read_stamps(out, n));
-  return 0;
-}
-
-int f5h_attn_force_variant(int32_t v) {
-  if (v != -1 && (v < 1 || v > 9) && (v < 21 || v > 27))
-    return fail(F5H_EINVAL, "attention variant must be -1, 1..9, 21..27");
-  attn_force_variant(v);
   g_kernel_epoch.fetch_add(1);
   return 0;
 }
@@ -1085,6 +1086,7 @@ int f5h_op_attention(void* stream, int32_t compute, int32_t S, int32_t H, int32_
                      const float* V, const int32_t* kv_len, int32_t q_prescaled, float* O, void* workspace,
                      size_t workspace_bytes) {
   if (S <= 0 || H <= 0 || N <= 0) return fail(F5H_EINVAL, "bad attention shape");
+  if (compute < F5H_FP32 || compute > F5H_FP16) return fail(F5H_EINVAL, "bad compute mode");
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   const int64_t n = (int64_t)S * H * N * 64;
   AttnArgs at{};
@@ -1099,15 +1101,15 @@ int f5h_op_attention(void* stream, int32_t compute, int32_t S, int32_t H, int32_
     if (workspace_bytes < need) return fail(F5H_ENOMEM, "workspace too small for op_attention");
     char* w = reinterpret_cast<char*>(workspace);
     void *q = w, *k = w + n * 2, *v = w + n * 4, *o = w + n * 6;
-    HIPCK(f32_to_op(1, Q, n, q, st));
-    HIPCK(f32_to_op(1, K, n, k, st));
-    HIPCK(f32_to_op(1, V, n, v, st));
+    HIPCK(f32_to_op(compute, Q, n, q, st));
+    HIPCK(f32_to_op(compute, K, n, k, st));
+    HIPCK(f32_to_op(compute, V, n, v, st));
     at.q = q;
     at.k = k;
     at.v = v;
     at.o = o;
-    HIPCK(attention(1, at, st));
-    HIPCK(op_to_f32(1, o, n, O, st));
+    HIPCK(attention(compute, at, st));
+    HIPCK(op_to_f32(compute, o, n, O, st));
   } else {
     at.q = Q;
     at.k = K;

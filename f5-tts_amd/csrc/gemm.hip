@@ -64,6 +64,11 @@ F5H_DEV void store8<bf16>(bf16* p, const V8& x) {
               f2bf(x.v[4]), f2bf(x.v[5]), f2bf(x.v[6]), f2bf(x.v[7])};
   *reinterpret_cast<bf16x8*>(p) = b;
 }
+template <>
+F5H_DEV void store8<f16>(f16* p, const V8& x) {
+  f16x8 b = {(f16)x.v[0], (f16)x.v[1], (f16)x.v[2], (f16)x.v[3], (f16)x.v[4], (f16)x.v[5], (f16)x.v[6], (f16)x.v[7]};
+  *reinterpret_cast<f16x8*>(p) = b;
+}
 F5H_DEV V8 load8(const float* p) {
   float4 a = *reinterpret_cast<const float4*>(p), b = *reinterpret_cast<const float4*>(p + 4);
   return V8{{a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w}};
@@ -130,7 +135,7 @@ F5H_DEV void epi8(const GemmArgs& g, int row, int col, V8 x, const V8* pre = nul
 #pragma unroll
     for (int e = 0; e < 8; ++e)
       x.v[e] = EPI == EPI_GELU_ERF_OP ? gelu_erf(x.v[e])
-                                      : (std::is_same<TC, bf16>::value ? gelu_tanh_fast(x.v[e]) : gelu_tanh(x.v[e]));
+                                      : (is16<TC>() ? gelu_tanh_fast(x.v[e]) : gelu_tanh(x.v[e]));
     TC* C = reinterpret_cast<TC*>(g.C);
     if (full && g.ldc % 8 == 0) {
       store8<TC>(C + off, x);
@@ -281,7 +286,7 @@ __global__ __launch_bounds__(64 * WGM * WGN, 1) void gemm_kernel(GemmArgs g) {
   // oldest VMEM ops, retired by the first stage wait), so the epilogue's read-modify-write does
   // not expose a dependent HBM/MALL round trip. Register budget: small tiles only.
   constexpr int CH_ = WN / 8, TPS = 16 * CH_ / 64;
-  constexpr bool PREF = EPI == EPI_RESID && std::is_same<TC, bf16>::value && (16 * CH_) % 64 == 0 &&
+  constexpr bool PREF = EPI == EPI_RESID && is16<TC>() && (16 * CH_) % 64 == 0 &&
                         MT * TPS * 8 <= 32;
   V8 pre[PREF ? MT : 1][PREF ? TPS : 1];
   if constexpr (PREF) {
@@ -349,16 +354,6 @@ __global__ __launch_bounds__(64 * WGM * WGN, 1) void gemm_kernel(GemmArgs g) {
         acc[i][j] = Slab<TC>::mma(__builtin_bit_cast(frag, ar[1][i]), __builtin_bit_cast(frag, br[1][j]), acc[i][j]);
   }
   __syncthreads();
-  if (g.diag_skip_epilogue) {  // diagnostic timing build path: keep the accumulators live
-    float x = 0.f;
-#pragma unroll
-    for (int i = 0; i < MT; ++i)
-#pragma unroll
-      for (int j = 0; j < NT; ++j) x += acc[i][j][0];
-    if (x == 12345.678f) reinterpret_cast<float*>(g.C)[0] = x;
-    probe_exit(g.probe, probe_t);
-    return;
-  }
 
   // ---- epilogue, per wave and 16-row strip: accumulators -> the wave's LDS strip (fp32,
   // padded rows) -> 8-column chunks of whole rows, so the epilogue's global accesses are
@@ -477,7 +472,7 @@ __global__ __launch_bounds__(64 * WGM * WGN, 1) void gemm_kernel(GemmArgs g) {
 #pragma unroll
               for (int e = 0; e < 8; ++e)
                 x.v[e] = EPI == EPI_GELU_ERF_OP ? gelu_erf(x.v[e])
-                                                : (std::is_same<TC, bf16>::value ? gelu_tanh_fast(x.v[e]) : gelu_tanh(x.v[e]));
+                                                : (is16<TC>() ? gelu_tanh_fast(x.v[e]) : gelu_tanh(x.v[e]));
               store8<TC>(reinterpret_cast<TC*>(g.C) + (int64_t)row * g.ldc + col, x);
             } else {  // EPI_STORE
               store8<float>(reinterpret_cast<float*>(g.C) + (int64_t)row * g.ldc + col, x);
@@ -562,7 +557,7 @@ struct PPCfg {
   static_assert(bytes <= 160 * 1024, "LDS");
 };
 
-template <typename TC, int EPI, int BM, int BN, int WGM2, int WGN2, int KS, int D, int ABL = 0>
+template <typename TC, int EPI, int BM, int BN, int WGM2, int WGN2, int KS, int D>
 __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(GemmArgs g) {
   const ProbeT probe_t = probe_enter(g.probe);
   typedef PPCfg<BM, BN, WGM2, WGN2, KS, D> C;
@@ -578,14 +573,14 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(GemmArgs g) {
   const int nwg = gridDim.x, b = blockIdx.x, xq = nwg >> 3, xr = nwg & 7, xcd = b & 7;
   const int bid = (xcd < xr ? xcd * (xq + 1) : xr * (xq + 1) + (xcd - xr) * xq) + (b >> 3);
   const int m0 = (bid / ntn) * BM, n0 = (bid % ntn) * BN;
-  const bf16* A = reinterpret_cast<const bf16*>(g.A);
-  const bf16* W = reinterpret_cast<const bf16*>(g.W);
+  const TC* A = reinterpret_cast<const TC*>(g.A);
+  const TC* W = reinterpret_cast<const TC*>(g.W);
 
   // ---- DMA: group 0 stages the A rows, group 1 the W rows. Instruction i of wave w4 covers
   // rows (i*4 + w4)*16 .. +15 of its operand; lane -> (row = lane>>2, physical chunk lane&3).
   constexpr int NI = NA > NB ? NA : NB;
   const int nI = grp == 0 ? NA : NB;
-  const bf16* src[NI];
+  const TC* src[NI];
   uint32_t dst_off[NI];
 #pragma unroll
   for (int i = 0; i < NI; ++i) {
@@ -664,8 +659,8 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(GemmArgs g) {
   if (grp == 1) __builtin_amdgcn_s_barrier();  // group 1 sits out half-period 0
   for (int p = 0; p < nph; ++p) {
     // ---- mem(p): fragments of phase p, DMA of phase p+2, wait for own part of phase p+1
-    if constexpr (!(ABL & 4)) read_phase(p);
-    if constexpr (!(ABL & 1)) if (p + D < nph) dma_phase(p + D);
+    read_phase(p);
+    if (p + D < nph) dma_phase(p + D);
     wait_dma(p + 1, min(p + D, nph - 1));
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 #pragma unroll
@@ -678,18 +673,15 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(GemmArgs g) {
     __builtin_amdgcn_sched_barrier(0);
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
-    // ---- mma(p) (ABL 16: s_setprio 1 around the MFMA cluster, guide T5 — measurement variant)
-    if constexpr ((ABL & 16) != 0) __builtin_amdgcn_s_setprio(1);
-    if constexpr (!(ABL & 2))
+    // ---- mma(p)
+    typedef typename Op16<TC>::v8 v8;
 #pragma unroll
     for (int s = 0; s < KS; ++s)
 #pragma unroll
       for (int i = 0; i < MT; ++i)
 #pragma unroll
         for (int j = 0; j < NT; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, af[s][i]),
-                                                              __builtin_bit_cast(bf16x8, bfr[s][j]), acc[i][j], 0, 0, 0);
-    if constexpr ((ABL & 16) != 0) __builtin_amdgcn_s_setprio(0);
+          acc[i][j] = Op16<TC>::mma16(__builtin_bit_cast(v8, af[s][i]), __builtin_bit_cast(v8, bfr[s][j]), acc[i][j]);
     __builtin_amdgcn_sched_barrier(0);
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
@@ -715,11 +707,7 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(GemmArgs g) {
       const int row = rbase + i * 16 + rr, col = cbase + cc * 8;
       const float* sp = Cs + rr * C::EPAD + cc * 8;
       float4 x0 = *reinterpret_cast<const float4*>(sp), x1 = *reinterpret_cast<const float4*>(sp + 4);
-      if constexpr (ABL & 8) {
-        asm volatile("" ::"v"(x0.x), "v"(x0.y), "v"(x0.z), "v"(x0.w), "v"(x1.x), "v"(x1.y), "v"(x1.z), "v"(x1.w));
-      } else {
-        if (row < g.M && col < g.N) epi8<TC, EPI>(g, row, col, V8{{x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w}});
-      }
+      if (row < g.M && col < g.N) epi8<TC, EPI>(g, row, col, V8{{x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w}});
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
@@ -728,48 +716,21 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(GemmArgs g) {
   probe_exit(g.probe, probe_t);
 }
 
-static int gemm_abl() {  // ablation probe (tools): 1 no DMA, 2 no MFMA, 4 no LDS reads in the K loop
-  static int v = [] {
-    const char* e = getenv("F5H_GEMM_ABL");
-    return e ? atoi(e) : 0;
-  }();
-  return v;
-}
-
 template <typename TC, int EPI, int BM, int BN, int WGM2, int WGN2, int KS, int D>
 static void launch_pp(const GemmArgs& a, hipStream_t st) {
   const int tiles = ((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN);
-#define F5H_PP(X) hipLaunchKernelGGL((gemm_pp_kernel<TC, EPI, BM, BN, WGM2, WGN2, KS, D, X>), dim3(tiles), dim3(512), 0, st, a)
-  if constexpr (EPI == EPI_STORE) {
-    switch (gemm_abl()) {
-      case 1: F5H_PP(1); return;
-      case 2: F5H_PP(2); return;
-      case 3: F5H_PP(3); return;
-      case 4: F5H_PP(4); return;
-      case 5: F5H_PP(5); return;
-      case 6: F5H_PP(6); return;
-      case 7: F5H_PP(7); return;
-      case 8: F5H_PP(8); return;
-      case 15: F5H_PP(15); return;
-      case 16: F5H_PP(16); return;
-      default: break;
-    }
-  }
-  F5H_PP(0);
-#undef F5H_PP
+  hipLaunchKernelGGL((gemm_pp_kernel<TC, EPI, BM, BN, WGM2, WGN2, KS, D>), dim3(tiles), dim3(512), 0, st, a);
 }
 
-// Tile configurations (bf16; the fp32 parity mode always uses cfg 0):
+// Tile configurations (16-bit operands; the fp32 parity mode always uses cfg 0):
 //   0: 64x128,  4 waves (2x2, 32x64 each),  3 stages, 2 blocks/CU
 //   1: 128x128, 4 waves (2x2, 64x64 each),  2 stages, 2 blocks/CU
-//   2: 128x256, 8 waves (2x4, 64x64 each),  3 stages, 1 block/CU
-//   3: 192x256, 8 waves (2x4, 96x64 each),  2 stages, 1 block/CU
-//   4: 256x128, 8 waves (4x2, 64x64 each),  3 stages, 1 block/CU
 //   5: 192x128, 4 waves (2x2, 96x64 each),  2 stages, 2 blocks/CU
-//   6: 128x128, 8 waves (4x2, 32x64 each),  3 stages, 1 block/CU
-//   7: 256x256, 8 waves (2x4, 128x64 each), 2 stages, 1 block/CU
+//  11: 256x256 ping-pong, 8 waves as two groups of 4, 3-phase ring, 1 block/CU
+// (round 1 also measured 128x256, 192x256, 256x128, 256x256 4-wave forms and seven other
+// ping-pong geometries; none won a shape, so they are no longer built — DESIGN.md §3.)
 // Per-CU LDS-DMA intake (~37 B/clk) bounds the small tiles: bytes per MFLOP staged =
-// 64*(BM+BN)/(BM*BN) KB, so 64x128 -> 24, 128x256 -> 12, 192x256 -> 9.3.
+// 64*(BM+BN)/(BM*BN) KB, so 64x128 -> 24, 128x128 -> 16, 256x256 -> 8.
 static int g_force_cfg = -1;
 static int gemm_env_cfg() {
   static int v = [] {
@@ -839,37 +800,23 @@ template <typename TC, int EPI>
 static hipError_t launch_t(const GemmArgs& a, hipStream_t st) {
   if (a.M == 0) return hipSuccess;
   int cfg = 0;
-  if constexpr (std::is_same<TC, bf16>::value) {
+  if constexpr (is16<TC>()) {
     cfg = g_force_cfg >= 0 ? g_force_cfg : gemm_env_cfg();
     if (cfg < 0) cfg = gemm_map_cfg(a.N, a.K);
     if (cfg < 0) cfg = pick_cfg(a);
   }
   switch (cfg) {
-    case 1: launch_cfg<TC, EPI, 128, 128, 2, 2, 2>(a, st); break;
-    case 2: launch_cfg<TC, EPI, 128, 256, 2, 4, 3>(a, st); break;
-    case 3: launch_cfg<TC, EPI, 192, 256, 2, 4, 2>(a, st); break;
-    case 4: launch_cfg<TC, EPI, 256, 128, 4, 2, 3>(a, st); break;
-    case 5: launch_cfg<TC, EPI, 192, 128, 2, 2, 2>(a, st); break;
-    case 6: launch_cfg<TC, EPI, 128, 128, 4, 2, 3>(a, st); break;
-    case 7: launch_cfg<TC, EPI, 256, 256, 2, 4, 2>(a, st); break;
     case 0: launch_cfg<TC, EPI, 64, 128, 2, 2, 3>(a, st); break;
-    default:
-      if constexpr (std::is_same<TC, bf16>::value) {
-        if (a.K % 64) return hipErrorInvalidValue;  // ping-pong configs: whole K64 phases
-        switch (cfg) {
-          case 10: launch_pp<TC, EPI, 256, 256, 1, 4, 1, 2>(a, st); break;
-          case 11: launch_pp<TC, EPI, 256, 256, 1, 4, 1, 3>(a, st); break;
-          case 12: launch_pp<TC, EPI, 256, 192, 1, 4, 1, 3>(a, st); break;
-          case 13: launch_pp<TC, EPI, 256, 192, 1, 4, 1, 4>(a, st); break;
-          case 14: launch_pp<TC, EPI, 256, 128, 2, 2, 1, 4>(a, st); break;
-          case 15: launch_pp<TC, EPI, 256, 128, 2, 2, 2, 2>(a, st); break;
-          case 16: launch_pp<TC, EPI, 128, 128, 2, 2, 2, 3>(a, st); break;
-          case 17: launch_pp<TC, EPI, 128, 128, 2, 2, 1, 6>(a, st); break;
-          default: return hipErrorInvalidValue;
-        }
-      } else {
-        return hipErrorInvalidValue;
+    case 1: launch_cfg<TC, EPI, 128, 128, 2, 2, 2>(a, st); break;
+    case 5: launch_cfg<TC, EPI, 192, 128, 2, 2, 2>(a, st); break;
+    case 11:
+      if constexpr (is16<TC>()) {
+        if (a.K % 64) return hipErrorInvalidValue;  // ping-pong: whole K64 phases
+        launch_pp<TC, EPI, 256, 256, 1, 4, 1, 3>(a, st);
+        break;
       }
+      return hipErrorInvalidValue;
+    default: return hipErrorInvalidValue;
   }
   return hipGetLastError();
 }
@@ -892,16 +839,17 @@ static hipError_t launch_epi(int epi, const GemmArgs& a, hipStream_t st) {
 
 void gemm_force_config(int cfg) { g_force_cfg = cfg; }
 
-hipError_t gemm(int compute, int epi, const GemmArgs& a_in, hipStream_t st) {
-  static const int diag = [] { const char* e = getenv("F5H_GEMM_DIAG"); return e ? atoi(e) : 0; }();
-  GemmArgs a = a_in;
-  a.diag_skip_epilogue = diag == 1 ? 1 : 0;
+hipError_t gemm(int compute, int epi, const GemmArgs& a, hipStream_t st) {
   const int bke = compute ? 64 : 32;
   if (a.K % bke != 0 || a.M < 0 || a.N <= 0 || a.lda % 8 || a.ldw % 8) return hipErrorInvalidValue;
   // 8-column epilogue chunks: vector paths need 16 B alignment of every operand row
   if (epi == EPI_INPROJ && (a.ldc % 8 || a.ld_add % 8 || a.N % 8)) return hipErrorInvalidValue;
   if (epi == EPI_QKV && (a.N % 64)) return hipErrorInvalidValue;
-  return compute ? launch_epi<bf16>(epi, a, st) : launch_epi<float>(epi, a, st);
+  switch (compute) {
+    case F5H_C_BF16: return launch_epi<bf16>(epi, a, st);
+    case F5H_C_FP16: return launch_epi<f16>(epi, a, st);
+    default: return launch_epi<float>(epi, a, st);
+  }
 }
 
 }  // namespace f5h

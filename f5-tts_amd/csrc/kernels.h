@@ -5,6 +5,10 @@
 
 namespace f5h {
 
+// Operand dtype of a compute mode (f5h_compute in include/f5h.h): GEMM/attention/conv operands are
+// fp32 (parity mode), bf16 or fp16; accumulation, residual stream, norms and the ODE state stay fp32.
+enum ComputeMode { F5H_C_FP32 = 0, F5H_C_BF16 = 1, F5H_C_FP16 = 2 };
+
 enum Epi {
   EPI_STORE = 0,      // C = acc + bias                                  (fp32 out)
   EPI_SILU = 1,       // C = silu(acc + bias)                            (fp32 out)
@@ -47,12 +51,11 @@ struct GemmArgs {
   void* q; void* k; void* v;
   float q_scale;                   // EPI_QKV: q is stored pre-multiplied by this (0 -> 1)
   DevProbe probe;                  // in-kernel launch timing (null slots: off)
-  int diag_skip_epilogue;          // diagnostics only (F5H_GEMM_DIAG=1): no epilogue, results invalid
 };
 
-// compute: 0 fp32 operands, 1 bf16 operands. A and W both in the operand dtype.
+// compute: ComputeMode (fp32 / bf16 / fp16 operands). A and W both in the operand dtype.
 hipError_t gemm(int compute, int epi, const GemmArgs& a, hipStream_t st);
-// pin the bf16 GEMM tile configuration (-1 = automatic choice); tuning and test hook
+// pin the 16-bit GEMM tile configuration (0, 1, 5, 11; -1 = automatic choice); tuning and test hook
 void gemm_force_config(int cfg);
 
 // attention: Q,K,V [S,H,L,64] operand dtype; O [S,L,H*64] operand dtype.
@@ -65,9 +68,6 @@ struct AttnArgs {
   DevProbe probe;         // in-kernel launch timing (null slots: off)
 };
 hipError_t attention(int compute, const AttnArgs& a, hipStream_t st);
-// pin the bf16 attention variant (-1 = default); tuning and test hook
-void attn_force_variant(int v);
-hipError_t attn_read_stamps(uint64_t* host, int n);  // variant 6 diagnostic stamps
 
 // grouped conv1d k=31, 16 groups, pad 15 (ConvPositionEmbedding, modules.py:175-201)
 struct ConvArgs {
@@ -109,9 +109,11 @@ hipError_t dwconv_ln(int compute, const float* x, int S, int L, int C, const flo
 // GRN: sumsq[s,c] = sum_n x^2 ; then out = gamma*(x*Nx)+beta+x -> operand dtype
 hipError_t grn(int compute, const float* x, int S, int L, int C, const float* gamma, const float* beta,
                float* scratch /*[(ceil(L/64)+1)*S*C]*/, void* out, hipStream_t st);
-// A_ct [S*N, 128 + td] operand dtype: [where(cond_mask,cond,0) (zeros for uncond) pad 128 | text]
+// A_ct [S*N, 128 + td] operand dtype: [where(cond_mask,cond,0) (zeros for uncond) pad 128 | text];
+// drop_audio / drop_text apply to the first (conditional) B sequences (single-branch forward)
 hipError_t build_ct(int compute, const float* cond, const uint8_t* cond_mask, const float* text_c,
-                    const float* text_u, int B, int N, int td, int S, void* out, hipStream_t st);
+                    const float* text_u, int B, int N, int td, int S, int drop_audio, int drop_text, void* out,
+                    hipStream_t st);
 // y (fp32 [B,N,mel]) -> ypad operand [B*N, 128]
 hipError_t pack_y(int compute, const float* y, int rows, int mel, void* ypad, hipStream_t st);
 // CFG + Euler: y += dt * (pc + (pc - pu) * cfg); pred rows from p with row offset/stride.

@@ -19,7 +19,8 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("F5H_LIB", os.path.join(_HERE, "lib", "libf5h.so"))
 
 F5H_DIT, F5H_UNETT = 0, 1
-F5H_FP32, F5H_BF16 = 0, 1
+F5H_FP32, F5H_BF16, F5H_FP16 = 0, 1, 2
+COMPUTE = {"fp32": F5H_FP32, "bf16": F5H_BF16, "fp16": F5H_FP16}
 
 # exported symbols, checked by tests/test_boundary.py against include/f5h.h
 EXPORTS = (
@@ -35,8 +36,6 @@ EXPORTS = (
     "f5h_op_linear",
     "f5h_op_attention",
     "f5h_gemm_force_config",
-    "f5h_attn_force_variant",
-    "f5h_debug_attn_stamps",
     "f5h_vocos_create",
     "f5h_vocos_destroy",
     "f5h_vocos_workspace_size",
@@ -87,6 +86,7 @@ class ForwardArgs(ctypes.Structure):
         ("x", ctypes.c_void_p), ("cond", ctypes.c_void_p), ("cond_mask", ctypes.c_void_p),
         ("text", ctypes.c_void_p), ("duration", ctypes.c_void_p), ("t", ctypes.c_float),
         ("use_batch_mask", ctypes.c_int32), ("pred", ctypes.c_void_p),
+        ("cfg_infer", ctypes.c_int32), ("drop_audio_cond", ctypes.c_int32), ("drop_text", ctypes.c_int32),
     ]
 
 
@@ -131,10 +131,6 @@ def lib():
     L.f5h_op_attention.restype = ctypes.c_int
     L.f5h_gemm_force_config.argtypes = [i32]
     L.f5h_gemm_force_config.restype = ctypes.c_int
-    L.f5h_attn_force_variant.argtypes = [i32]
-    L.f5h_attn_force_variant.restype = ctypes.c_int
-    L.f5h_debug_attn_stamps.argtypes = [vp, i32]
-    L.f5h_debug_attn_stamps.restype = ctypes.c_int
     L.f5h_vocos_create.argtypes = [ctypes.POINTER(VocosArch), ctypes.POINTER(Weight), i32, i32, ctypes.POINTER(vp)]
     L.f5h_vocos_create.restype = ctypes.c_int
     L.f5h_vocos_destroy.argtypes = [vp]

@@ -3,8 +3,9 @@
 
 Same rules as the reference:
   * dtype default: fp16 when the device is a GPU of compute capability >= 7 (every ROCm device here),
-    else fp32 (utils_infer.py:189-196). On this engine fp16 parameters select the bf16 MFMA mode
-    (CFM.engine_compute "auto"); fp32 parameters select the exact-fp32 parity mode.
+    else fp32 (utils_infer.py:189-196). On this engine fp16 parameters select the fp16 MFMA mode
+    (CFM.engine_compute "auto": the reference's own GPU arithmetic), bf16 parameters the bf16 mode
+    and fp32 parameters the exact-fp32 parity mode.
   * `.safetensors` via safetensors (no code execution), anything else via
     torch.load(weights_only=True) (utils_infer.py:198-204).
   * use_ema: the EMA state ("ema_model_state_dict", or the whole safetensors file) with the

@@ -27,7 +27,7 @@ def _arch_struct(arch: dict, compute: str) -> _lib.Arch:
     a.text_mask_padding = int(bool(arch.get("text_mask_padding", True)))
     a.pe_attn_head = int(arch.get("pe_attn_head") or 0)
     a.attn_mask_enabled = int(bool(arch.get("attn_mask_enabled", False)))
-    a.compute = {"fp32": _lib.F5H_FP32, "bf16": _lib.F5H_BF16}[compute]
+    a.compute = _lib.COMPUTE[compute]
     if arch.get("qk_norm"):
         raise NotImplementedError("qk_norm is not used by any shipped config (F5TTS_*.yaml qk_norm: null)")
     if arch.get("long_skip_connection") or arch.get("text_embedding_average_upsampling"):
@@ -147,8 +147,11 @@ class Engine:
                        "f5h_sample")
         return out, traj
 
-    def forward(self, x, cond, cond_mask, text, duration, t: float, use_batch_mask):
-        """One packed cond/uncond backbone forward -> pred [2B,N,mel] (DiT.forward(cfg_infer=True))."""
+    def forward(self, x, cond, cond_mask, text, duration, t: float, use_batch_mask, cfg_infer=True,
+                drop_audio_cond=False, drop_text=False):
+        """One backbone forward at time t (DiT.forward / UNetT.forward, dit.py:319-370).
+        cfg_infer: packed cond/uncond -> pred [2B,N,mel]; else one branch -> [B,N,mel] honouring
+        drop_audio_cond / drop_text."""
         B, N, mel = x.shape
         nt = text.shape[1]
         x = x.to(self.device, torch.float32).contiguous()
@@ -156,8 +159,9 @@ class Engine:
         cmask = cond_mask.to(self.device, torch.uint8).contiguous()
         text = text.to(self.device, torch.int64).contiguous()
         dur = duration.to(self.device, torch.int32).contiguous()
-        pred = torch.empty(2 * B, N, mel, dtype=torch.float32, device=self.device)
-        ws = self._workspace(self.workspace_bytes(B, N, nt, 1, True))
+        S = 2 * B if cfg_infer else B
+        pred = torch.empty(S, N, mel, dtype=torch.float32, device=self.device)
+        ws = self._workspace(self.workspace_bytes(B, N, nt, 1, cfg_infer))
         a = _lib.ForwardArgs()
         a.B, a.N, a.nt = B, N, nt
         a.x, a.cond, a.cond_mask, a.text, a.duration = (x.data_ptr(), cond.data_ptr(), cmask.data_ptr(),
@@ -165,6 +169,9 @@ class Engine:
         a.t = float(t)
         a.use_batch_mask = int(bool(use_batch_mask))
         a.pred = pred.data_ptr()
+        a.cfg_infer = int(bool(cfg_infer))
+        a.drop_audio_cond = int(bool(drop_audio_cond))
+        a.drop_text = int(bool(drop_text))
         with torch.cuda.device(self.device):
             _lib.check(_lib.lib().f5h_forward(self._h, _lib.stream_handle(self.device), ctypes.byref(a),
                                               ws.data_ptr(), ws.numel()), "f5h_forward")
@@ -191,10 +198,9 @@ def op_linear(A, W, bias=None, compute="bf16"):
     N = W.shape[0]
     C = torch.empty(M, N, dtype=torch.float32, device=A.device)
     ws = torch.empty(((N + 127) // 128 * 128) * K * 4 + 512 + M * K * 4, dtype=torch.uint8, device=A.device)
-    c = {"fp32": 0, "bf16": 1}[compute]
-    _lib.check(_lib.lib().f5h_op_linear(_lib.stream_handle(A.device), c, M, N, K, A.contiguous().data_ptr(),
-                                        W.contiguous().data_ptr(), _lib.ptr(bias), C.data_ptr(), ws.data_ptr(),
-                                        ws.numel()), "f5h_op_linear")
+    _lib.check(_lib.lib().f5h_op_linear(_lib.stream_handle(A.device), _lib.COMPUTE[compute], M, N, K,
+                                        A.contiguous().data_ptr(), W.contiguous().data_ptr(), _lib.ptr(bias),
+                                        C.data_ptr(), ws.data_ptr(), ws.numel()), "f5h_op_linear")
     return C
 
 
@@ -204,20 +210,14 @@ def op_attention(Q, K, V, kv_len=None, compute="bf16", q_prescaled=False):
     assert D == 64
     O = torch.empty(S, N, H * 64, dtype=torch.float32, device=Q.device)
     ws = torch.empty(Q.numel() * 8 + 1024, dtype=torch.uint8, device=Q.device)
-    c = {"fp32": 0, "bf16": 1}[compute]
     kv = None if kv_len is None else kv_len.to(Q.device, torch.int32).contiguous()
-    _lib.check(_lib.lib().f5h_op_attention(_lib.stream_handle(Q.device), c, S, H, N, Q.contiguous().data_ptr(),
-                                           K.contiguous().data_ptr(), V.contiguous().data_ptr(), _lib.ptr(kv),
-                                           int(bool(q_prescaled)), O.data_ptr(), ws.data_ptr(), ws.numel()),
-               "f5h_op_attention")
+    _lib.check(_lib.lib().f5h_op_attention(_lib.stream_handle(Q.device), _lib.COMPUTE[compute], S, H, N,
+                                           Q.contiguous().data_ptr(), K.contiguous().data_ptr(),
+                                           V.contiguous().data_ptr(), _lib.ptr(kv), int(bool(q_prescaled)),
+                                           O.data_ptr(), ws.data_ptr(), ws.numel()), "f5h_op_attention")
     return O
 
 
 def gemm_force_config(cfg: int = -1):
-    """Pin the bf16 GEMM tile configuration (0..7, 10..17) for this process; -1 = automatic."""
+    """Pin the 16-bit GEMM tile configuration (0, 1, 5, 11) for this process; -1 = automatic."""
     _lib.check(_lib.lib().f5h_gemm_force_config(int(cfg)), "gemm_force_config")
-
-
-def attn_force_variant(v: int = -1):
-    """Pin the bf16 attention kernel variant (1, 2, 3) for this process; -1 = default."""
-    _lib.check(_lib.lib().f5h_attn_force_variant(int(v)), "attn_force_variant")

@@ -19,6 +19,16 @@ from ... import configs
 from ._params import build_param_tree, rotary_inv_freq
 
 
+def compute_for_dtype(dtype: torch.dtype) -> str:
+    """Engine compute mode for a parameter dtype: fp32 -> exact-f32 parity mode, fp16 -> fp16 MFMA
+    operands (the reference's GPU default, utils_infer.py:190-199), bf16 -> bf16 MFMA operands."""
+    if dtype == torch.float16:
+        return "fp16"
+    if dtype == torch.bfloat16:
+        return "bf16"
+    return "fp32"
+
+
 class EngineBackbone(nn.Module):
     backbone_name = "DiT"
 
@@ -36,7 +46,9 @@ class EngineBackbone(nn.Module):
 
     # ------------------------------------------------------------------ engine cache
     def _weights_version(self):
-        return tuple(p._version for p in self.parameters()) + (id(self),)
+        # _version misses writes through .data (p.data.copy_); the storage pointer and dtype catch
+        # re-assigned / re-cast parameters, so a stale packed engine is never reused
+        return tuple((p._version, p.data_ptr(), p.dtype) for p in self.parameters()) + (id(self),)
 
     def engine_weights(self) -> dict:
         return {k: v for k, v in self.state_dict().items() if not k.endswith("inv_freq")}
@@ -78,19 +90,36 @@ class EngineBackbone(nn.Module):
     # ------------------------------------------------------------------ plugin forward
     def forward(self, x, cond, text, time, mask=None, drop_audio_cond=False, drop_text=False, cfg_infer=False,
                 cache=False, compute: str | None = None):
-        """Packed cond/uncond forward through the engine (the path CFM.sample uses, cfm.py:181-191).
-        `cond` must already be the masked step_cond; returns [2B, N, mel]."""
-        if not cfg_infer:
-            raise NotImplementedError("engine backbones implement the packed CFG forward (cfg_infer=True); "
-                                      "single-branch sampling runs inside CFM.sample")
+        """DiT.forward / UNetT.forward through the engine (dit.py:319-370, unett.py:244-307).
+
+        cfg_infer=True: the packed cond/uncond forward of CFM.sample (cfm.py:181-191) -> [2B, N, mel];
+        cfg_infer=False: one branch (cfm.py:167-178) -> [B, N, mel], honouring drop_audio_cond and
+        drop_text. `cond` is the already-masked step_cond; `time` a scalar or one value per sample
+        (dit.py:332-333 repeats a scalar; distinct values run as groups of equal t, which is exact
+        because sequences of equal padded length N are independent in the backbone). `cache` has no
+        effect: the engine recomputes the text embedding per call (the reference's cache only avoids
+        recomputing it)."""
         B, N = x.shape[:2]
-        if torch.is_tensor(time) and time.numel() > 1:
-            if not bool((time == time.reshape(-1)[0]).all()):
-                raise NotImplementedError("per-sample time values are not used by CFM.sample")
-        t = float(time.reshape(-1)[0]) if torch.is_tensor(time) else float(time)
-        compute = compute or ("fp32" if next(self.parameters()).dtype == torch.float32 else "bf16")
+        compute = compute or compute_for_dtype(next(self.parameters()).dtype)
         eng = self.get_engine(compute, x.device)
         dur = mask.sum(1) if mask is not None else torch.full((B,), N, device=x.device)
         ones = torch.ones(B, N, dtype=torch.uint8, device=x.device)
-        pred = eng.forward(x, cond, ones, text, dur, t, use_batch_mask=mask is not None)
+        use_mask = mask is not None
+        tv = time.reshape(-1).float().cpu() if torch.is_tensor(time) else torch.tensor([float(time)])
+        if tv.numel() not in (1, B):
+            raise ValueError(f"time must be a scalar or have one value per sample ({B}), got {tv.numel()}")
+        flags = dict(cfg_infer=cfg_infer, drop_audio_cond=drop_audio_cond, drop_text=drop_text)
+        values = torch.unique(tv)
+        if values.numel() == 1:
+            pred = eng.forward(x, cond, ones, text, dur, float(values[0]), use_mask, **flags)
+            return pred.to(x.dtype)
+        S = 2 * B if cfg_infer else B
+        pred = torch.empty(S, N, x.shape[2], dtype=torch.float32, device=x.device)
+        for v in values.tolist():
+            idx = torch.nonzero(tv == v).flatten().to(x.device)
+            p = eng.forward(x[idx], cond[idx], ones[idx], text[idx], dur[idx], v, use_mask, **flags)
+            nb = idx.numel()
+            pred[idx] = p[:nb]
+            if cfg_infer:
+                pred[idx + B] = p[nb:]
         return pred.to(x.dtype)

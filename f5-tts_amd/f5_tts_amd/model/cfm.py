@@ -43,16 +43,22 @@ class CFM(nn.Module):
         self.sigma = sigma
         self.odeint_kwargs = odeint_kwargs
         self.vocab_char_map = vocab_char_map
-        self.compute = compute  # "auto" | "bf16" | "fp32"
+        if compute not in ("auto", "fp32", "bf16", "fp16"):
+            raise ValueError(f"compute must be 'auto', 'fp32', 'bf16' or 'fp16', got {compute!r}")
+        self.compute = compute
 
     @property
     def device(self):
         return next(self.parameters()).device
 
     def engine_compute(self) -> str:
+        """"auto": the parameter dtype picks the mode (fp32 -> parity, fp16 -> fp16 MFMA as the reference
+        runs on GPUs, utils_infer.py:190-199; bf16 -> bf16 MFMA); or "fp32" / "bf16" / "fp16" explicitly."""
         if self.compute != "auto":
             return self.compute
-        return "fp32" if next(self.parameters()).dtype == torch.float32 else "bf16"
+        from .backbones.base import compute_for_dtype
+
+        return compute_for_dtype(next(self.parameters()).dtype)
 
     @torch.no_grad()
     def sample(self, cond, text, duration, *, lens=None, steps=32, cfg_strength=1.0, sway_sampling_coef=None,
@@ -63,8 +69,6 @@ class CFM(nn.Module):
         initial noise explicitly (parity tests), `keep_trajectory=False` skips the [steps+1,...] copy."""
         if self.training:
             self.eval()
-        if duplicate_test:
-            raise NotImplementedError("duplicate_test is a debugging corner of the reference (cfm.py:141-143)")
         pdtype = next(self.parameters()).dtype
         if cond.ndim == 2:  # raw wave -> mel (cfm.py:106-109)
             cond = self.mel_spec(cond)
@@ -95,6 +99,9 @@ class CFM(nn.Module):
         else:  # == F.pad(lens_to_mask(lens), ...) below: max_duration > lens.amax() by the rule above
             cond_mask = lens_to_mask(lens, length=max_duration)
 
+        if duplicate_test:  # inner-time-step observation corner (cfm.py:141-143)
+            test_cond = F.pad(cond, (0, 0, cond_seq_len, max_duration - 2 * cond_seq_len), value=0.0)
+
         cond = F.pad(cond, (0, 0, 0, max_duration - cond_seq_len), value=0.0)
         if no_ref_audio:
             cond = torch.zeros_like(cond)
@@ -109,8 +116,14 @@ class CFM(nn.Module):
                 ys.append(torch.randn(dur, self.num_channels, device=self.device, dtype=pdtype))
             y0 = pad_sequence(ys, padding_value=0, batch_first=True)
 
+        t_start = 0.0
+        if duplicate_test:  # cfm.py:205-209
+            t_start = t_inter
+            y0 = (1 - t_start) * y0 + t_start * test_cond
+            steps = int(steps * (1 - t_start))
+
         # the grid is a host constant of the call: built on the CPU in the parameter dtype (cfm.py:211-216)
-        t = time_grid(steps, sway_sampling_coef, use_epss, device="cpu", dtype=pdtype)
+        t = time_grid(steps, sway_sampling_coef, use_epss, device="cpu", dtype=pdtype, t_start=t_start)
         t_host = t.float().numpy()
 
         eng = self.transformer.get_engine(self.engine_compute(), self.device)

@@ -10,6 +10,11 @@ utterances. This module holds the two host-side pieces around that:
 * `gather_mels`: the only collective on the path — an all-gather of per-rank counts and
   lengths, then of the finished mels (padded to the max per rank), over RCCL (backend
   "nccl") on GPUs or gloo on CPU.
+* `run_sharded`: the job driver that strings them together the way the reference's eval driver
+  does (eval_infer_batch.py:178-214: barrier, split the prompts over processes, per batch
+  `model.sample(cond, text, duration, lens, ...)`, keep `gen[ref_len:total_len]`, barrier), with
+  LPT sharding and length buckets instead of a count split, and the finished mels gathered to
+  every rank instead of written to per-utterance files.
 """
 
 from __future__ import annotations
@@ -75,3 +80,48 @@ def gather_mels(local: "dict[int, torch.Tensor]", device=None, group=None):
             if k >= 0:
                 out[k] = b[j, :n].clone()
     return out
+
+
+def padded_mel_batch(mels, length=None):
+    """[n_i, C] mels -> [B, max n_i (or length), C], zero padded (utils_eval.py:58-66, frame-major)."""
+    n = max(m.shape[0] for m in mels) if length is None else length
+    out = mels[0].new_zeros(len(mels), n, mels[0].shape[-1])
+    for i, m in enumerate(mels):
+        out[i, : m.shape[0]] = m
+    return out
+
+
+def plan(totals, world: int, max_batch: int):
+    """Per rank, the list of batches (utterance index lists): LPT over ranks, then length buckets."""
+    return [bucket(idx, totals, max_batch) for idx in shard_lpt(totals, world)]
+
+
+def run_sharded(utts, sample_fn, *, rank: int, world: int, max_batch: int = 32, device=None, group=None,
+                batches=None):
+    """Run a whole utterance job data-parallel and return {index: generated mel [total-ref, C]} on
+    every rank.
+
+    utts: list of dicts with `cond` [ref_i(, padded), C] mel, `text` (str list or id list), `ref` (prompt
+    frames) and `total` (total frames), the fields of one prompt in eval_infer_batch.py:182-185.
+    sample_fn(cond [B,Nc,C], text list, duration LongTensor[B], lens LongTensor[B]) -> out [B,N,C]: the
+    engine's `CFM.sample` (or a stand-in in tests). `batches` (from `plan`) may be passed to reuse a
+    plan across calls. World 1 runs without any collective."""
+    if batches is None:
+        batches = plan([u["total"] for u in utts], world, max_batch)[rank]
+    local = {}
+    for b in batches:
+        cond = padded_mel_batch([utts[i]["cond"][: utts[i]["ref"]] for i in b])
+        if device is not None:
+            cond = cond.to(device)
+        text = [utts[i]["text"] for i in b]
+        if torch.is_tensor(text[0]):  # token ids: one [B, nt] LongTensor, -1 padded (list_str_to_idx layout)
+            text = torch.nn.utils.rnn.pad_sequence(text, batch_first=True, padding_value=-1).to(cond.device)
+        dur = torch.tensor([utts[i]["total"] for i in b], dtype=torch.long, device=cond.device)
+        lens = torch.tensor([utts[i]["ref"] for i in b], dtype=torch.long, device=cond.device)
+        out = sample_fn(cond, text, dur, lens)
+        for j, i in enumerate(b):
+            local[i] = out[j, utts[i]["ref"]: utts[i]["total"]]
+    if world == 1:
+        return local
+    return gather_mels(local, device=device, group=group)
+

@@ -37,7 +37,13 @@ enum f5h_status {
 };
 
 enum f5h_backbone { F5H_DIT = 0, F5H_UNETT = 1 };
-enum f5h_compute { F5H_FP32 = 0, F5H_BF16 = 1 };
+/* Operand dtype of the GEMM / attention / conv MFMAs. Accumulation, the residual stream, norms,
+ * softmax statistics and the ODE state are fp32 in every mode.
+ *   F5H_FP32: parity mode (exact-f32 MFMA, VALU attention), the <=1e-3 contract;
+ *   F5H_BF16: bf16 operands (the BASELINE configs' dtype);
+ *   F5H_FP16: fp16 operands = the reference's default GPU dtype (load_checkpoint casts to fp16 on
+ *             any GPU with compute capability >= 7, utils_infer.py:190-199); same MFMA rate as bf16. */
+enum f5h_compute { F5H_FP32 = 0, F5H_BF16 = 1, F5H_FP16 = 2 };
 
 /* Architecture: mirrors DiT.__init__ (dit.py:171-192) / UNetT.__init__ (unett.py:108-129)
  * and the Hydra arch block (configs/F5TTS_v1_Base.yaml:24-37). */
@@ -55,7 +61,7 @@ typedef struct f5h_arch {
   int32_t text_mask_padding; /* 0/1 */
   int32_t pe_attn_head;      /* 0 = rope on all heads, k>0 = first k heads (modules.py:503-506) */
   int32_t attn_mask_enabled; /* 0/1: key-padding mask in attention (modules.py:512-516) */
-  int32_t compute;           /* f5h_compute: FP32 parity mode or BF16 MFMA mode */
+  int32_t compute;           /* f5h_compute: FP32 parity mode, BF16 or FP16 MFMA mode */
 } f5h_arch;
 
 /* One named parameter, host memory, float32, C-contiguous, with the reference's
@@ -103,9 +109,14 @@ size_t f5h_workspace_size(const f5h_engine* eng, int32_t B, int32_t N, int32_t n
 int f5h_sample(f5h_engine* eng, void* stream, const f5h_sample_args* args, void* workspace,
                size_t workspace_bytes);
 
-/* One packed backbone forward (DiT.forward / UNetT.forward with cfg_infer=True, cache=True):
- * x [B,N,mel], step_cond = where(cond_mask,cond,0) computed from cond/cond_mask, time t.
- * Writes pred [2B,N,mel] (cond rows then uncond rows). Used for op-level parity. */
+/* One backbone forward: the backbone plugin contract DiT.forward / UNetT.forward
+ * (dit.py:319-370, unett.py:244-307) with a scalar time t.
+ *   cfg_infer = 1: the packed cond/uncond forward CFM.sample uses (cfm.py:181-191): pred [2B,N,mel],
+ *                  conditional rows then unconditional rows (drop flags ignored);
+ *   cfg_infer = 0: one branch (cfm.py:167-178), pred [B,N,mel], honouring drop_audio_cond (cond -> 0,
+ *                  InputEmbedding, dit.py:155-156) and drop_text (all-filler text ids, dit.py:106-107).
+ * x [B,N,mel]; step_cond = where(cond_mask, cond, 0) is formed from cond/cond_mask. Per-sample time
+ * values are served by the caller in groups of equal t (sequences are independent at equal N). */
 typedef struct f5h_forward_args {
   int32_t B, N, nt;
   const float* x;
@@ -115,24 +126,31 @@ typedef struct f5h_forward_args {
   const int32_t* duration;
   float t;
   int32_t use_batch_mask;
-  float* pred;               /* [2B,N,mel] */
+  float* pred;               /* [2B,N,mel] (cfg_infer) or [B,N,mel] */
+  int32_t cfg_infer;
+  int32_t drop_audio_cond;
+  int32_t drop_text;
 } f5h_forward_args;
 int f5h_forward(f5h_engine* eng, void* stream, const f5h_forward_args* args, void* workspace,
                 size_t workspace_bytes);
 
-/* Kernel probe: when enabled the engine brackets every launch of kernel class `kclass`
- * with HIP events on the launch stream; f5h_probe_read returns (launches, total ms).
- * Classes: 0 = FFN1 GEMM, 1 = attention, 2 = QKV GEMM, 3 = FFN2 GEMM, 4 = conv,
- * 5 = attention output-projection GEMM, 6 = pre-FFN norm (LayerNorm+modulate / RMSNorm). */
+/* Kernel probe: when enabled, every launch of kernel class `kclass` is timed on the device wall
+ * clock (s_memrealtime): GEMM and attention kernels stamp their own entry/exit, the other classes
+ * get a stamp kernel on each side (no HIP events, so it also times graph replays; every 4th NFE
+ * step is sampled). f5h_probe_read returns (sampled launches, total ms). Enabling resets the slots
+ * and synchronises the device. Classes: 0 = FFN1 GEMM, 1 = attention, 2 = QKV GEMM, 3 = FFN2 GEMM,
+ * 4 = conv, 5 = attention output-projection GEMM, 6 = pre-FFN norm (LayerNorm+modulate / RMSNorm). */
 int f5h_probe_enable(f5h_engine* eng, int32_t kclass, int32_t enable);
 int f5h_probe_read(f5h_engine* eng, int64_t* launches, double* total_ms);
 
 /* NFE-step graph (the CFM.sample ODE loop, cfm.py:218 -> torchdiffeq Euler): with mode 1 (default;
  * env F5H_GRAPH=0 selects 0 at engine creation) f5h_sample captures one NFE step -- table-row
  * copy, backbone forward, CFG combine + Euler update, device step counter -- into a hipGraph on
- * first use for a (workspace, out, trajectory, B, N, nfe, cfg, mask, probe) key and replays it
- * nfe times; mode 0 launches the same sequence eagerly. Results are bitwise identical.
- * f5h_graph_stats: captures so far, step replays so far, graphs cached (LRU, at most 8). */
+ * first use and replays it nfe times; mode 0 launches the same sequence eagerly. The step touches
+ * only workspace buffers, so the graph is keyed by (workspace, B, N, nfe, cfg, mask, probe,
+ * kernel epoch); the caller's out/trajectory pointers are staged into the workspace per call.
+ * Results are bitwise identical in both modes. f5h_graph_stats: captures so far, step replays so
+ * far, graphs cached (LRU, at most 8; an evicted graph is destroyed only after its last user). */
 int f5h_set_graph_mode(f5h_engine* eng, int32_t mode);
 int f5h_graph_stats(f5h_engine* eng, int64_t* captures, int64_t* replays, int32_t* cached);
 
@@ -147,15 +165,9 @@ int f5h_op_attention(void* stream, int32_t compute, int32_t S, int32_t H, int32_
                      const float* K, const float* V, const int32_t* kv_len, int32_t q_prescaled, float* O,
                      void* workspace, size_t workspace_bytes);
 
-/* Tuning/test hook: pin the bf16 GEMM tile configuration for all later launches in this
- * process (0..7, 10..17), or -1 to restore the automatic per-shape choice. */
+/* Tuning/test hook: pin the 16-bit GEMM tile configuration for all later launches in this
+ * process (0, 1, 5, 11), or -1 to restore the automatic per-shape choice. */
 int f5h_gemm_force_config(int32_t cfg);
-/* Tuning/test hook: pin the bf16 attention kernel variant (1, 2, 3), or -1
- * to restore the default. */
-int f5h_attn_force_variant(int32_t variant);
-/* Diagnostic: per-segment cycle sums of the last variant-6 attention launch (first 4 (s,head)
- * pairs x 8 waves x 8 words). */
-int f5h_debug_attn_stamps(uint64_t* out, int32_t n);
 
 /* ---------------------------------------------------------------------------------------
  * Vocos decoder (mel -> waveform), SURVEY §8(f1): the step after the CFM path, replacing

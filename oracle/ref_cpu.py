@@ -47,12 +47,13 @@ EPSS = {  # model/utils.py:207-214
 }
 
 
-def epss_sway_grid(steps: int, sway, use_epss=True, dtype=torch.float32):
-    """Time grid: EPSS table /32 (or linspace), then t += s*(cos(pi/2 t) - 1 + t)."""
-    if use_epss and steps in EPSS:
+def epss_sway_grid(steps: int, sway, use_epss=True, dtype=torch.float32, t_start=0.0):
+    """Time grid (cfm.py:211-216): EPSS table /32 when t_start == 0 (else linspace(t_start, 1)),
+    then t += s*(cos(pi/2 t) - 1 + t)."""
+    if t_start == 0 and use_epss and steps in EPSS:
         t = (1 / 32) * torch.tensor(EPSS[steps], dtype=dtype)
     else:
-        t = torch.linspace(0, 1, steps + 1, dtype=dtype)
+        t = torch.linspace(t_start, 1, steps + 1, dtype=dtype)
     if sway is not None:
         t = t + sway * (torch.cos(torch.pi / 2 * t) - 1 + t)
     return t
@@ -211,9 +212,10 @@ def dit_block(W, i, arch, x, t_emb, mask, rope):
     return x + g2[:, None] * ffn(W, p + "ff.", f)
 
 
-def dit_forward(W, arch, x, cond, text, t, mask, text_cache, packed=True):
+def dit_forward(W, arch, x, cond, text, t, mask, text_cache, packed=True, drop_audio=False, drop_text=False):
     """Packed cond/uncond DiT forward (cfg_infer=True, cache=True). Returns [2b,n,mel].
-    `packed=False`: the single conditional forward of `cfm.py:167-178` (drop flags False) -> [b,n,mel]."""
+    `packed=False`: one branch (dit.py:347-350) honouring drop_audio / drop_text -> [b,n,mel]
+    (the forward of `cfm.py:167-178` is the one with both flags False)."""
     b, n = x.shape[:2]
     t = t.reshape(-1).expand(b) if t.numel() == 1 else t
     te = time_embed(W, t)
@@ -221,14 +223,15 @@ def dit_forward(W, arch, x, cond, text, t, mask, text_cache, packed=True):
         seq = n if mask is None else mask.sum(1)
         text_cache["cond"] = text_embed_dit(W, arch, text, seq, False)
         text_cache["uncond"] = text_embed_dit(W, arch, text, seq, True)
-    xc = input_embed(W, x, cond, text_cache["cond"], False, mask)
     if packed:
+        xc = input_embed(W, x, cond, text_cache["cond"], False, mask)
         xu = input_embed(W, x, cond, text_cache["uncond"], True, mask)
         h = torch.cat((xc, xu), 0)
         te = torch.cat((te, te), 0)
         m2 = None if mask is None else torch.cat((mask, mask), 0)
     else:
-        h, m2 = xc, mask
+        h = input_embed(W, x, cond, text_cache["uncond" if drop_text else "cond"], drop_audio, mask)
+        m2 = mask
     rope = rope_cos_sin(n, arch["dim_head"])
     for i in range(arch["depth"]):
         h = dit_block(W, i, arch, h, te, m2, rope)
@@ -253,21 +256,22 @@ def text_embed_unett(W, arch, text, n, drop_text):
     return W["text_embed.text_embed.weight"][text]  # conv_layers=0 for E2 Base
 
 
-def unett_forward(W, arch, x, cond, text, t, mask, text_cache, packed=True):
+def unett_forward(W, arch, x, cond, text, t, mask, text_cache, packed=True, drop_audio=False, drop_text=False):
     b, n = x.shape[:2]
     t = t.reshape(-1).expand(b) if t.numel() == 1 else t
     te = time_embed(W, t)
     if "cond" not in text_cache:
         text_cache["cond"] = text_embed_unett(W, arch, text, n, False)
         text_cache["uncond"] = text_embed_unett(W, arch, text, n, True)
-    xc = input_embed(W, x, cond, text_cache["cond"], False, None)  # no mask (unett.py:90-102)
-    if packed:
+    if packed:  # InputEmbedding takes no mask (unett.py:90-102)
+        xc = input_embed(W, x, cond, text_cache["cond"], False, None)
         xu = input_embed(W, x, cond, text_cache["uncond"], True, None)
         h = torch.cat((xc, xu), 0)
         te = torch.cat((te, te), 0)
         m2 = None if mask is None else torch.cat((mask, mask), 0)
     else:
-        h, m2 = xc, mask
+        h = input_embed(W, x, cond, text_cache["uncond" if drop_text else "cond"], drop_audio, None)
+        m2 = mask
     h = torch.cat((te[:, None], h), 1)
     if m2 is not None:
         m2 = F.pad(m2, (1, 0), value=True)
@@ -313,9 +317,12 @@ def prepare(arch, cond, text, duration, lens=None, max_duration=65536, edit_mask
 @torch.no_grad()
 def cfm_sample(W, arch, cond, text, duration, *, lens=None, steps=32, cfg_strength=1.0,
                sway_sampling_coef=None, y0=None, seed=None, use_epss=True, edit_mask=None,
-               max_steps=None, no_ref_audio=False):
+               max_steps=None, no_ref_audio=False, duplicate_test=False, t_inter=0.1):
     """fp32 restatement of CFM.sample. `y0` overrides the noise recipe (cfm.py:196-201).
-    `max_steps` truncates the Euler loop (used only for bounded CPU-baseline timing)."""
+    `max_steps` truncates the Euler loop (used only for bounded CPU-baseline timing).
+    duplicate_test (cfm.py:141-143, 205-209): start at t_inter from a mix of the noise and the prompt
+    shifted by its own length, over int(steps * (1 - t_inter)) linspace steps."""
+    cond_len = cond.shape[1]
     pre = prepare(arch, cond.float(), text, duration, lens, edit_mask=edit_mask, no_ref_audio=no_ref_audio)
     if y0 is None:
         from torch.nn.utils.rnn import pad_sequence
@@ -335,7 +342,13 @@ def cfm_sample(W, arch, cond, text, duration, *, lens=None, steps=32, cfg_streng
         pc, pu = torch.chunk(p, 2, 0)
         return pc + (pc - pu) * cfg_strength
 
-    t = epss_sway_grid(steps, sway_sampling_coef, use_epss)
+    t_start = 0.0
+    if duplicate_test:
+        test_cond = F.pad(cond.float(), (0, 0, cond_len, pre["N"] - 2 * cond_len), value=0.0)
+        t_start = t_inter
+        y0 = (1 - t_start) * y0.float() + t_start * test_cond
+        steps = int(steps * (1 - t_start))
+    t = epss_sway_grid(steps, sway_sampling_coef, use_epss, t_start=t_start)
     y = y0.float()
     traj = [y]
     n_run = steps if max_steps is None else min(steps, max_steps)

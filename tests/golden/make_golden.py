@@ -181,8 +181,9 @@ def run_edge(name, seed=7):
                 checksum=checksum(inp))
 
 
-def run_forward(arch, case, t_val=0.3, seed=7):
-    """One packed cond/uncond backbone forward at time t (dit.py:319-370 with cfg_infer=True)."""
+def run_forward(arch, case, t_val=0.3, seed=7, cfg_infer=True, drop_audio_cond=False, drop_text=False):
+    """One backbone forward at time t (dit.py:319-370): packed cond/uncond (cfg_infer=True) or one
+    branch with the drop flags; t_val a scalar or one value per sample."""
     model = build_ref(arch)
     inp = synthetic.make_case(**case)
     B = inp["cond"].shape[0]
@@ -195,7 +196,8 @@ def run_forward(arch, case, t_val=0.3, seed=7):
     mask = (torch.arange(N)[None] < dur[:, None]) if B > 1 else None
     with torch.no_grad():
         out = model.transformer(x=x, cond=step_cond, text=inp["text"], time=torch.tensor(t_val), mask=mask,
-                                cfg_infer=True, cache=True)
+                                cfg_infer=cfg_infer, drop_audio_cond=drop_audio_cond, drop_text=drop_text,
+                                cache=True)
         model.transformer.clear_cache()
     return out.float().numpy()
 
@@ -212,6 +214,9 @@ def main():
     install_shims()
     torch.set_num_threads(8)
 
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))  # tests/
+    import golden_cases as gc
+
     tiny = configs.get_arch("DiT_tiny", text_num_embeds=64)
     tiny_v0 = configs.get_arch("DiT_tiny", text_num_embeds=64, text_mask_padding=False, pe_attn_head=1)
     tiny_masked = configs.get_arch("DiT_tiny", text_num_embeds=64, attn_mask_enabled=True)
@@ -220,12 +225,10 @@ def main():
     b1 = dict(B=1, ref_frames=60, total_frames=150, n_text=30, vocab=64)
     b3 = dict(B=3, ref_frames=[40, 60, 25], total_frames=[90, 150, 70], n_text=[20, 30, 12], vocab=64)
 
-    jobs = {
-        "dit_tiny_fwd_b1": lambda: dict(out=run_forward(tiny, b1)),
-        "dit_tiny_fwd_b3": lambda: dict(out=run_forward(tiny, b3)),
-        "unett_tiny_fwd_b1": lambda: dict(out=run_forward(utiny, b1)),
-        "unett_tiny_fwd_b3": lambda: dict(out=run_forward(utiny, b3)),
-    }
+    jobs = {}
+    for name, (tag, spec, opts) in gc.FORWARD_CASES.items():
+        jobs[name] = (lambda a, sp, o: (lambda: dict(out=run_forward(a, sp, **gc.forward_ref_kwargs(o)))))(
+            gc.arch_of(tag), spec, opts)
 
     def sample_job(arch, case, nfe, **kw):
         def f():
@@ -243,14 +246,22 @@ def main():
     c1_case = dict(B=1, ref_frames=282, total_frames=564, n_text=90)
     for dt, tag in ((torch.float32, "fp32"), (torch.bfloat16, "bf16"), (torch.float16, "fp16")):
         jobs[f"c1_sample_{tag}"] = sample_job(c1, c1_case, 4, dtype=dt)
-    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))  # tests/
-    import golden_cases as gc
-
     for name in gc.EDGE_CASES:
         jobs[name] = (lambda n: (lambda: run_edge(n)))(name)
+    # Base-size cases (round 2): E2 UNetT Base (C5 architecture) and the F5 v1 Base batch path, both at
+    # reduced NFE and frame counts so the CPU reference finishes in seconds; fp32.
+    e2 = configs.get_arch("E2TTS_Base")
+    base = configs.get_arch("F5TTS_v1_Base")
+    base_masked = configs.get_arch("F5TTS_v1_Base", attn_mask_enabled=True)
+    jobs["e2_base_sample_b2"] = sample_job(e2, gc.E2B2, 2)
+    jobs["base_batch_sample_b4"] = sample_job(base, gc.BASE_B4, 2)
+    jobs["base_batch_sample_b4_masked"] = sample_job(base_masked, gc.BASE_B4, 2)
     if not args.skip_c2:
         c2 = configs.get_arch("F5TTS_v1_Base")
-        jobs["c2_sample_fp32"] = sample_job(c2, dict(B=1, ref_frames=938, total_frames=1876, n_text=300), 16)
+        jobs["c2_sample_fp32"] = sample_job(c2, gc.C2, 16)
+        # the reference's own reduced-precision envelopes at C2 (same fp32 y0)
+        jobs["c2_sample_bf16"] = sample_job(c2, gc.C2, 16, dtype=torch.bfloat16)
+        jobs["c2_sample_fp16"] = sample_job(c2, gc.C2, 16, dtype=torch.float16)
 
     # time grids (model/utils.py:205-218 + cfm.py:215-216), computed by the reference itself
     from f5_tts.model.utils import get_epss_timesteps

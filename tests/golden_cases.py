@@ -18,6 +18,10 @@ B1 = dict(B=1, ref_frames=60, total_frames=150, n_text=30, vocab=64)
 B3 = dict(B=3, ref_frames=[40, 60, 25], total_frames=[90, 150, 70], n_text=[20, 30, 12], vocab=64)
 C1 = dict(B=1, ref_frames=282, total_frames=564, n_text=90)
 C2 = dict(B=1, ref_frames=938, total_frames=1876, n_text=300)
+# Base-size cases (fp32 fixtures, reduced NFE/frames): E2 UNetT Base (the C5 architecture, its skip-proj
+# GEMMs and ff 4096) and the F5 v1 Base batch path (C3's mask semantics at Base dimensions).
+E2B2 = dict(B=2, ref_frames=[100, 60], total_frames=[300, 220], n_text=[50, 40])
+BASE_B4 = dict(B=4, ref_frames=[120, 200, 80, 150], total_frames=[400, 520, 260, 450], n_text=[60, 90, 40, 70])
 
 
 def arch_of(tag):
@@ -33,6 +37,10 @@ def arch_of(tag):
         return configs.get_arch("F5TTS_v1_Small_4L")
     if tag == "c2":
         return configs.get_arch("F5TTS_v1_Base")
+    if tag == "c2_masked":
+        return configs.get_arch("F5TTS_v1_Base", attn_mask_enabled=True)
+    if tag == "e2":
+        return configs.get_arch("E2TTS_Base")
     raise KeyError(tag)
 
 
@@ -47,17 +55,37 @@ SAMPLE_CASES = {
     "unett_tiny_sample_b3": ("utiny", B3, 4, -1.0, 2.0),
     "c1_sample_fp32": ("c1", C1, 4, -1.0, 2.0),
     "c2_sample_fp32": ("c2", C2, 16, -1.0, 2.0),
+    "e2_base_sample_b2": ("e2", E2B2, 2, -1.0, 2.0),
+    "base_batch_sample_b4": ("c2", BASE_B4, 2, -1.0, 2.0),
+    "base_batch_sample_b4_masked": ("c2_masked", BASE_B4, 2, -1.0, 2.0),
 }
 
+# Backbone-plugin forwards (DiT.forward / UNetT.forward, dit.py:319-370): name -> (arch tag, input
+# spec, options). Options: cfg_infer (default True: packed cond/uncond), drop_audio / drop_text (single
+# branch), t (scalar or one value per sample; default FWD_T).
 FORWARD_CASES = {
-    "dit_tiny_fwd_b1": ("tiny", B1),
-    "dit_tiny_fwd_b3": ("tiny", B3),
-    "unett_tiny_fwd_b1": ("utiny", B1),
-    "unett_tiny_fwd_b3": ("utiny", B3),
+    "dit_tiny_fwd_b1": ("tiny", B1, {}),
+    "dit_tiny_fwd_b3": ("tiny", B3, {}),
+    "unett_tiny_fwd_b1": ("utiny", B1, {}),
+    "unett_tiny_fwd_b3": ("utiny", B3, {}),
+    "dit_tiny_fwd_b3_single": ("tiny", B3, {"cfg_infer": False}),
+    "dit_tiny_fwd_b3_dropaudio": ("tiny", B3, {"cfg_infer": False, "drop_audio": True}),
+    "dit_tiny_fwd_b3_droptext": ("tiny", B3, {"cfg_infer": False, "drop_text": True}),
+    "dit_tiny_fwd_b1_dropboth": ("tiny", B1, {"cfg_infer": False, "drop_audio": True, "drop_text": True}),
+    "dit_tiny_fwd_b3_tvec": ("tiny", B3, {"t": [0.1, 0.7, 0.1]}),
+    "unett_tiny_fwd_b3_droptext": ("utiny", B3, {"cfg_infer": False, "drop_text": True}),
+    "unett_tiny_fwd_b3_tvec_single": ("utiny", B3, {"cfg_infer": False, "t": [0.9, 0.2, 0.5]}),
 }
+
 
 SEED = 7
 FWD_T = 0.3
+
+
+def forward_ref_kwargs(opts):
+    """make_golden.run_forward keyword arguments of a FORWARD_CASES option dict."""
+    return dict(t_val=opts.get("t", FWD_T), cfg_infer=opts.get("cfg_infer", True),
+                drop_audio_cond=opts.get("drop_audio", False), drop_text=opts.get("drop_text", False))
 
 
 def load(name):
@@ -88,6 +116,7 @@ def max_rel(a, b):
 #          no_ref   -> no_ref_audio=True (cfm.py:146-147)
 #          int_dur  -> duration passed as a python int (cfm.py:132-139 rule then lifts it per utterance)
 #          epss     -> use_epss flag
+#          dup      -> duplicate_test=True with t_inter = value (cfm.py:141-143, 205-209)
 SHORT = dict(B=1, ref_frames=3, total_frames=5, n_text=2, vocab=64)
 EDGE_CASES = {
     "edge_dit_nocfg_b1": ("tiny", B1, 4, -1.0, 0.0, {}),
@@ -99,6 +128,8 @@ EDGE_CASES = {
     "edge_dit_nfe1_b1": ("tiny", B1, 1, None, 2.0, {}),
     "edge_dit_short_b1": ("tiny", SHORT, 3, -1.0, 2.0, {}),
     "edge_dit_lin7_b3": ("tiny", B3, 7, 0.5, 1.5, {"epss": False}),
+    "edge_dit_duptest_b1": ("tiny", B1, 8, -1.0, 2.0, {"dup": 0.1}),
+    "edge_dit_duptest_b3": ("tiny", dict(B3, total_frames=[90, 150, 130]), 6, None, 2.0, {"dup": 0.25}),
 }
 
 
@@ -121,4 +152,7 @@ def edge_sample_kwargs(inp, extra):
         kw["no_ref_audio"] = True
     if "epss" in extra:
         kw["use_epss"] = extra["epss"]
+    if "dup" in extra:
+        kw["duplicate_test"] = True
+        kw["t_inter"] = extra["dup"]
     return kw

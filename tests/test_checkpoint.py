@@ -59,7 +59,8 @@ def test_raw_checkpoint_and_default_dtype(tmp_path):
     assert next(m.parameters()).dtype == torch.float32  # CPU device -> fp32 (utils_infer.py:189-196)
     assert m.engine_compute() == "fp32"
     m16 = m.to(torch.float16)
-    assert m16.engine_compute() == "bf16"  # the reference's fp16 GPU rule selects the bf16 MFMA mode
+    assert m16.engine_compute() == "fp16"  # the reference's fp16 GPU rule selects the fp16 MFMA mode
+    assert m.to(torch.bfloat16).engine_compute() == "bf16"
 
 
 def test_missing_key_is_an_error(tmp_path):

@@ -1,0 +1,300 @@
+"""Round-2 GPU coverage: the backbone plugin contract driven the way the reference's CFM drives it,
+the fp16 compute mode against the reference's own fp16 error, the C5 architecture at full size, and
+the graph cache / step-count boundaries. Every engine call goes through the C ABI (ctypes).
+
+Tolerances (written here):
+  * fp32 engine vs reference fp32 output: max|diff| / max|ref| <= 1e-3 (north star).
+  * bf16 / fp16 engine vs reference fp32: rel-L2 over the generated frames <= 1.5 x the reference's
+    own bf16 / fp16 error vs its fp32 output on the same inputs.
+"""
+
+import threading
+
+import numpy as np
+import pytest
+import torch
+
+import golden_cases as gc
+from f5_tts_amd import configs, synthetic
+from f5_tts_amd.model import CFM, DiT, UNetT
+from f5_tts_amd.model.utils import lens_to_mask, time_grid
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda:0"
+FP32_TOL = 1e-3
+
+
+def _need_gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+
+
+def _model(arch, compute):
+    cls = DiT if arch["backbone"] == "DiT" else UNetT
+    kw = {k: v for k, v in arch.items() if k not in ("backbone", "text_num_embeds", "mel_dim")}
+    net = cls(**kw, text_num_embeds=arch["text_num_embeds"], mel_dim=arch["mel_dim"])
+    net.load_state_dict(synthetic.make_weights_torch(arch), strict=False)
+    return CFM(transformer=net, num_channels=100, compute=compute).to(DEV)
+
+
+def _plugin_euler(backbone, inp, duration, nfe, cfg, sway, y0, use_epss=True):
+    """CFM.sample's host preamble and ODE loop written as the reference writes them (cfm.py:111-223:
+    step_cond, batch mask, fixed-grid Euler, the cfg < 1e-5 single-branch call and the packed CFG call),
+    with every forward going through the engine-backed backbone plugin."""
+    cond, text, lens = inp["cond"].to(DEV), inp["text"].to(DEV), inp["lens"].to(DEV)
+    B, cond_len = cond.shape[:2]
+    duration = torch.as_tensor(duration).to(DEV).expand(B)
+    duration = torch.maximum(torch.maximum((text != -1).sum(-1), lens) + 1, duration)
+    N = int(duration.max())
+    cond_mask = lens_to_mask(lens, length=N)[..., None]
+    cond = torch.nn.functional.pad(cond, (0, 0, 0, N - cond_len))
+    step_cond = torch.where(cond_mask, cond, torch.zeros_like(cond))
+    mask = lens_to_mask(duration) if B > 1 else None
+    t = time_grid(nfe, sway, use_epss, device=DEV, dtype=torch.float32)
+    y = y0.to(DEV)
+    traj = [y]
+    for k in range(nfe):
+        if cfg < 1e-5:
+            f = backbone(x=y, cond=step_cond, text=text, time=t[k], mask=mask, drop_audio_cond=False,
+                         drop_text=False, cache=True)
+        else:
+            pc = backbone(x=y, cond=step_cond, text=text, time=t[k], mask=mask, cfg_infer=True, cache=True)
+            p, null = torch.chunk(pc, 2, dim=0)
+            f = p + (p - null) * cfg
+        y = y + (t[k + 1] - t[k]) * f
+        traj.append(y)
+    backbone.clear_cache()
+    return torch.where(cond_mask, cond, y), torch.stack(traj)
+
+
+# ---------------------------------------------------------------- backbone plugin contract
+@pytest.mark.parametrize("name", ["edge_dit_nocfg_b1", "edge_dit_nocfg_b3", "edge_unett_nocfg_b3"])
+def test_plugin_single_branch_euler_loop_matches_reference(name):
+    """The reference's cfg < 1e-5 branch (cfm.py:167-178) calls the backbone with cfg_infer=False; a
+    Python Euler loop written like cfm.py:162-191 drives the engine plugin that way and matches the
+    reference's own CFM.sample output in fp32."""
+    _need_gpu()
+    g = gc.load(name)
+    tag, spec, nfe, sway, cfg, extra = gc.EDGE_CASES[name]
+    assert cfg == 0.0 and not extra
+    arch = gc.arch_of(tag)
+    m = _model(arch, "fp32")
+    inp = synthetic.make_case(**spec)
+    dur = torch.maximum(torch.maximum((inp["text"] != -1).sum(-1), inp["lens"]) + 1, inp["duration"])
+    y0 = synthetic.reference_noise(dur, gc.SEED)
+    out, traj = _plugin_euler(m.transformer, inp, inp["duration"], nfe, cfg, sway, y0)
+    torch.cuda.synchronize()
+    assert gc.max_rel(traj[1].cpu().numpy(), g["traj_1"]) < FP32_TOL
+    assert gc.max_rel(out.cpu().numpy(), g["out"]) < FP32_TOL
+
+
+def test_plugin_packed_cfg_euler_loop_matches_reference():
+    """The CFG branch (cfm.py:181-191) through the plugin (cfg_infer=True, batch mask path)."""
+    _need_gpu()
+    name = "dit_tiny_sample_b3"
+    g = gc.load(name)
+    tag, spec, nfe, sway, cfg = gc.SAMPLE_CASES[name]
+    m = _model(gc.arch_of(tag), "fp32")
+    inp = synthetic.make_case(**spec)
+    dur = torch.maximum(torch.maximum((inp["text"] != -1).sum(-1), inp["lens"]) + 1, inp["duration"])
+    y0 = synthetic.reference_noise(dur, gc.SEED)
+    out, _ = _plugin_euler(m.transformer, inp, inp["duration"], nfe, cfg, sway, y0)
+    torch.cuda.synchronize()
+    assert gc.max_rel(out.cpu().numpy(), g["out"]) < FP32_TOL
+
+
+@pytest.mark.parametrize("compute", ["bf16", "fp16"])
+@pytest.mark.parametrize("tag", ["tiny", "utiny"])
+def test_plugin_drop_both_equals_packed_uncond_half(compute, tag):
+    """A single-branch forward with drop_audio_cond and drop_text is, row for row, the unconditional
+    half of the packed CFG forward (dit.py:341-343): bitwise, since every row is computed alike."""
+    _need_gpu()
+    m = _model(gc.arch_of(tag), compute)
+    inp = synthetic.make_case(**gc.B3)
+    dur = torch.maximum(torch.maximum((inp["text"] != -1).sum(-1), inp["lens"]) + 1, inp["duration"])
+    N = int(dur.max())
+    x = synthetic.reference_noise(dur, 3).to(DEV)
+    cond = torch.nn.functional.pad(inp["cond"], (0, 0, 0, N - inp["cond"].shape[1])).to(DEV)
+    mask = lens_to_mask(dur.to(DEV))
+    kw = dict(x=x, cond=cond, text=inp["text"].to(DEV), time=torch.tensor(0.4), mask=mask)
+    packed = m.transformer(**kw, cfg_infer=True)
+    single_c = m.transformer(**kw)
+    single_u = m.transformer(**kw, drop_audio_cond=True, drop_text=True)
+    assert single_u.shape == (3, N, 100)
+    assert torch.equal(single_u, packed[3:])
+    assert torch.equal(single_c, packed[:3])
+
+
+# ---------------------------------------------------------------- fp16 mode (a20)
+def _envelope(name_f32, name_lo, gen, compute, nfe_case):
+    f32, lo = gc.load(name_f32), gc.load(name_lo)
+    tag, spec, nfe, sway, cfg = gc.SAMPLE_CASES[nfe_case]
+    m = _model(gc.arch_of(tag), compute)
+    inp = synthetic.make_case(**spec)
+    dur = torch.maximum(torch.maximum((inp["text"] != -1).sum(-1), inp["lens"]) + 1, inp["duration"])
+    y0 = synthetic.reference_noise(dur, gc.SEED)
+    out, _ = m.sample(cond=inp["cond"].to(DEV), text=inp["text"].to(DEV), duration=inp["duration"].to(DEV),
+                      lens=inp["lens"].to(DEV), steps=nfe, cfg_strength=cfg, sway_sampling_coef=sway,
+                      y0=y0.to(DEV), keep_trajectory=False)
+    out = out.float().cpu().numpy()
+    e_ours = gc.rel_err(out[:, gen], f32["out"][:, gen])
+    e_ref = gc.rel_err(lo["out"][:, gen], f32["out"][:, gen])
+    return e_ours, e_ref
+
+
+@pytest.mark.parametrize("compute", ["bf16", "fp16"])
+def test_c2_within_reference_envelope(compute):
+    """C2 (F5TTS_v1_Base, NFE 16, 938+938 frames): the engine's bf16 / fp16 error vs the reference fp32
+    output is at most 1.5x the reference's OWN bf16 / fp16 error (fixtures c2_sample_{bf16,fp16})."""
+    _need_gpu()
+    e_ours, e_ref = _envelope("c2_sample_fp32", f"c2_sample_{compute}", slice(938, None), compute, "c2_sample_fp32")
+    assert e_ours <= 1.5 * e_ref, (e_ours, e_ref)
+
+
+def test_c1_fp16_within_reference_envelope():
+    _need_gpu()
+    e_ours, e_ref = _envelope("c1_sample_fp32", "c1_sample_fp16", slice(282, None), "fp16", "c1_sample_fp32")
+    assert e_ours <= 1.5 * e_ref, (e_ours, e_ref)
+
+
+def test_fp16_parameters_select_fp16_engine():
+    """load_checkpoint's fp16 GPU rule (utils_infer.py:190-199): a half-precision model runs the fp16
+    engine mode, and its result is close to the fp32 engine's."""
+    _need_gpu()
+    arch = gc.arch_of("tiny")
+    m = _model(arch, "auto").half()
+    assert m.engine_compute() == "fp16"
+    m32 = _model(arch, "fp32")
+    inp = synthetic.make_case(**gc.B3)
+    kw = dict(cond=inp["cond"].to(DEV), text=inp["text"].to(DEV), duration=inp["duration"].to(DEV),
+              lens=inp["lens"].to(DEV), steps=4, cfg_strength=2.0, sway_sampling_coef=-1.0, seed=5,
+              keep_trajectory=False)
+    dur = torch.maximum(torch.maximum((inp["text"] != -1).sum(-1), inp["lens"]) + 1, inp["duration"])
+    y0 = synthetic.reference_noise(dur, 5).to(DEV)
+    out16, _ = m.sample(**kw, y0=y0)
+    out32, _ = m32.sample(**kw, y0=y0)
+    assert out16.dtype == torch.float16
+    assert gc.rel_err(out16.float().cpu().numpy(), out32.cpu().numpy()) < 2e-2
+
+
+# ---------------------------------------------------------------- C5 at full size
+def test_c5_full_size_properties():
+    """C5 (E2 UNetT Base, B=8 x 1876 frames; 2 Euler steps, the property does not depend on NFE):
+    finite, the prompt region equals the cond exactly (cfm.py:223), and permuting the utterances
+    permutes the outputs bit for bit. Exercises the skip-proj GEMMs, ff 4096 and the 256x256 GEMM
+    configuration pick_cfg selects at these shapes."""
+    _need_gpu()
+    arch = configs.get_arch("E2TTS_Base")
+    m = _model(arch, "bf16")
+    c5 = synthetic.c5_case()
+    B = c5["B"]
+    # mixed prompt lengths so the permutation check sees different rows
+    ref = [938 - 40 * i for i in range(B)]
+    inp = synthetic.make_case(B=B, ref_frames=ref, total_frames=c5["total"], n_text=c5["nt"])
+    dur = torch.full((B,), c5["total"])
+    y0 = synthetic.reference_noise(dur, 11)
+    kw = dict(steps=2, cfg_strength=2.0, sway_sampling_coef=-1.0, keep_trajectory=False)
+    out, _ = m.sample(cond=inp["cond"].to(DEV), text=inp["text"].to(DEV), duration=dur.to(DEV),
+                      lens=inp["lens"].to(DEV), y0=y0.to(DEV), **kw)
+    perm = torch.randperm(B, generator=torch.Generator().manual_seed(0))
+    outp, _ = m.sample(cond=inp["cond"][perm].to(DEV), text=inp["text"][perm].to(DEV), duration=dur[perm].to(DEV),
+                       lens=inp["lens"][perm].to(DEV), y0=y0[perm].to(DEV), **kw)
+    assert out.shape == (B, 1876, 100)
+    assert torch.isfinite(out).all()
+    assert torch.equal(outp, out[perm.to(DEV)])
+    for i in range(B):
+        L = int(inp["lens"][i])
+        assert torch.equal(out[i, :L].cpu(), inp["cond"][i, :L])
+    gen = out[:, 938:].float()
+    assert 0.1 < gen.std().item() < 50.0
+
+
+# ---------------------------------------------------------------- graph cache and step bounds
+def test_graph_cache_eviction_under_concurrent_callers():
+    """More distinct shapes than the 8-entry step-graph cache, sampled from three host threads at
+    once (the reference's ThreadPoolExecutor over text chunks, utils_infer.py:540-547): graphs are
+    evicted while other threads replay theirs, and every result still equals the sequential one."""
+    _need_gpu()
+    m = _model(gc.arch_of("tiny"), "bf16")
+    lengths = [40 + 7 * i for i in range(12)]
+    cases = []
+    for i, n in enumerate(lengths):
+        inp = synthetic.make_case(B=1, ref_frames=n // 3, total_frames=n, n_text=8, vocab=64, seed=100 + i)
+        cases.append((inp, synthetic.reference_noise(inp["duration"], i)))
+
+    def run(inp, y0):
+        out, _ = m.sample(cond=inp["cond"].to(DEV), text=inp["text"].to(DEV), duration=inp["duration"].to(DEV),
+                          lens=inp["lens"].to(DEV), steps=4, cfg_strength=2.0, sway_sampling_coef=-1.0,
+                          y0=y0.to(DEV), keep_trajectory=False)
+        return out
+
+    ref = [run(*c).clone() for c in cases]
+    torch.cuda.synchronize()
+    errors, results = [], {}
+
+    def worker(w):
+        try:
+            s = torch.cuda.Stream()
+            with torch.cuda.stream(s):
+                for rep in range(2):
+                    for i in range(w, len(cases), 3):
+                        results[(w, rep, i)] = run(*cases[i]).clone()
+            s.synchronize()
+        except Exception as ex:  # surfaced below
+            errors.append(ex)
+
+    ts = [threading.Thread(target=worker, args=(w,)) for w in range(3)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join(timeout=120)
+    assert not errors, errors
+    assert len(results) == 2 * len(cases)
+    for (w, rep, i), r in results.items():
+        assert torch.equal(r, ref[i]), (w, rep, i)
+    eng = m.transformer.get_engine("bf16", m.device)
+    assert eng.graph_stats()["cached"] <= 8
+
+
+def test_nfe_512_runs_and_matches_oracle():
+    """The largest accepted step count (512: 513 grid points) runs and matches the CPU oracle; 513
+    is rejected before anything is enqueued."""
+    _need_gpu()
+    from oracle import ref_cpu
+
+    arch = gc.arch_of("tiny")
+    W = synthetic.make_weights_torch(arch)
+    m = _model(arch, "fp32")
+    inp = synthetic.make_case(B=1, ref_frames=20, total_frames=48, n_text=10, vocab=64)
+    dur = torch.maximum(torch.maximum((inp["text"] != -1).sum(-1), inp["lens"]) + 1, inp["duration"])
+    y0 = synthetic.reference_noise(dur, gc.SEED)
+    kw = dict(steps=512, cfg_strength=2.0, sway_sampling_coef=-1.0)
+    with torch.no_grad():
+        ref, _ = ref_cpu.cfm_sample(W, arch, inp["cond"], inp["text"], inp["duration"], lens=inp["lens"], y0=y0, **kw)
+    out, _ = m.sample(cond=inp["cond"].to(DEV), text=inp["text"].to(DEV), duration=inp["duration"].to(DEV),
+                      lens=inp["lens"].to(DEV), y0=y0.to(DEV), keep_trajectory=False, **kw)
+    torch.cuda.synchronize()
+    assert gc.max_rel(out.cpu().numpy(), ref.numpy()) < FP32_TOL
+    with pytest.raises(RuntimeError):
+        m.sample(cond=inp["cond"].to(DEV), text=inp["text"].to(DEV), duration=inp["duration"].to(DEV),
+                 lens=inp["lens"].to(DEV), y0=y0.to(DEV), keep_trajectory=False, **dict(kw, steps=513))
+
+
+@pytest.mark.parametrize("name", ["edge_dit_duptest_b1", "edge_dit_duptest_b3", "edge_dit_nocfg_b3"])
+def test_edge_sample_fp16(name):
+    """Edge paths of CFM.sample in the fp16 mode: rel-L2 <= 2e-2 against the reference fp32 output."""
+    _need_gpu()
+    g = gc.load(name)
+    tag, spec, nfe, sway, cfg, extra = gc.EDGE_CASES[name]
+    m = _model(gc.arch_of(tag), "fp16")
+    inp = synthetic.make_case(**spec)
+    kw = gc.edge_sample_kwargs(inp, extra)
+    dur = torch.as_tensor(kw["duration"]).expand(inp["lens"].shape[0])
+    dur = torch.maximum(torch.maximum((inp["text"] != -1).sum(-1), inp["lens"]) + 1, dur)
+    y0 = synthetic.reference_noise(dur, gc.SEED)
+    kw = {k: (v.to(DEV) if isinstance(v, torch.Tensor) else v) for k, v in kw.items()}
+    out, _ = m.sample(**kw, steps=nfe, cfg_strength=cfg, sway_sampling_coef=sway, y0=y0.to(DEV))
+    torch.cuda.synchronize()
+    assert np.asarray(out.shape).tolist() == list(g["out"].shape)
+    assert gc.rel_err(out.float().cpu().numpy(), g["out"]) < 2e-2
