@@ -97,7 +97,13 @@ struct f5h_engine {
   std::mutex gm;
   std::vector<std::shared_ptr<struct GraphEntry>> graphs;
   hipStream_t cap = nullptr;  // private capture stream (the caller's may be the null stream)
+  hipStream_t cap2 = nullptr; // second capture stream: the unconditional CFG branch
+  hipEvent_t ev_fork = nullptr, ev_join = nullptr;
   int graph_mode = 1;
+  // CFG branches as parallel captured chains: 2 = auto (batches of >= 4 utterances: C5 -4 % per call;
+  // at B = 1 the half-size launches cost more than the overlap gains, C2 +4 %), 1 = always, 0 = never
+  // (env F5H_SPLIT_CFG, f5h_set_cfg_streams)
+  int split_cfg = 2;
   uint64_t use_ctr = 0;
   int64_t n_captures = 0, n_replays = 0;
   // probe
@@ -123,12 +129,13 @@ static std::atomic<uint64_t> g_kernel_epoch{0};
 
 struct GraphKey {
   const void* ws;
-  int B, N, nfe, use_cfg, batch_mask, probe;
-  uint64_t kernel_epoch;  // bumped whenever a forced GEMM config / attention variant changes
+  int B, N, nfe, use_cfg, batch_mask, probe, split;
+  uint64_t kernel_epoch;  // bumped whenever a forced GEMM config changes
   uint32_t cfg_bits;
   bool operator==(const GraphKey& o) const {
     return ws == o.ws && B == o.B && N == o.N && nfe == o.nfe && kernel_epoch == o.kernel_epoch &&
-           use_cfg == o.use_cfg && batch_mask == o.batch_mask && probe == o.probe && cfg_bits == o.cfg_bits;
+           use_cfg == o.use_cfg && batch_mask == o.batch_mask && probe == o.probe && cfg_bits == o.cfg_bits &&
+           split == o.split;
   }
 };
 // Shared by the cache and by every call replaying it: an entry evicted while another thread is
@@ -494,6 +501,7 @@ struct Ctx {
   Bufs b;
   int B, N, nt, S, L, nfe, use_cfg, batch_mask;
   int drop_audio, drop_text;  // single-branch forward only (f5h_forward with cfg_infer = 0)
+  hipStream_t st2;            // second stream for the unconditional branch (step-graph capture), or null
   int site;  // probe launch-site counter, reset at the start of every step's enqueue
 };
 
@@ -594,106 +602,121 @@ static int step_prep(Ctx& c) {
   return 0;
 }
 
-// One packed cond/uncond backbone forward for the current step; result in b.p [S, L, mel].
-static int backbone_step(Ctx& c) {
+// Sequences [s0, s0+ns) of the packed cond/uncond backbone forward for the current step, enqueued
+// on `st`; result in b.p rows of those sequences. Every buffer is sequence-major, so a part works on
+// pointer offsets of the packed buffers; sequences never interact, so a part computes exactly what
+// the packed forward computes for its rows (bitwise: GEMM tile configurations agree bit for bit).
+static int backbone_part(Ctx& c, int s0, int ns, hipStream_t st) {
   f5h_engine* e = c.e;
   const f5h_arch& a = e->a;
   const int d = a.dim, bf = e->bf, H = a.heads, inner = H * 64;
   const bool dit = a.backbone == F5H_DIT;
+  const size_t es = e->esz;
   Bufs& b = c.b;
-  hipStream_t st = c.st;
   const int BN = c.B * c.N;
-  const int rows = c.S * c.L;
-  const uint8_t* keep = c.batch_mask ? b.rowkeep : nullptr;
-  // ---- input embedding: h0 = y.Wx^T + P (both branches), conv position embedding
+  const int rows = ns * c.L;
+  const size_t ro = (size_t)s0 * c.L;  // first row of the part (L rows per sequence)
+  const size_t no = (size_t)s0 * c.N;  // first row in the N-row input-embedding buffers
+  auto op = [&](void* base, size_t row, size_t width) -> void* { return (char*)base + row * width * es; };
+  const uint8_t* keep = c.batch_mask ? b.rowkeep + ro : nullptr;
+  float* bh = b.h + ro * d;
+  float* bh2 = b.h2 ? b.h2 + ro * d : nullptr;
+  void* aop = op(b.aop, ro, d);
+  void* q = op(b.q, ro, inner);
+  void* k = op(b.k, ro, inner);
+  void* v = op(b.v, ro, inner);
+  void* o = op(b.o, ro, inner);
+  void* f = op(b.f, ro, a.ff_dim);
+  // ---- input embedding: h0 = y.Wx^T + P, conv position embedding. Sequence s reads y[s % B]; a
+  // part holding both branches computes y.Wx^T once and adds both branches' hoisted P rows.
   {
-    GemmArgs g = gargs(b.ypad, 128, e->in_x, BN, b.h0, d);
+    GemmArgs g = gargs(b.ypad, 128, e->in_x, BN, b.h0 + no * d, d);
     g.bias = nullptr;
-    g.add = b.P;
+    g.add = b.P + no * d;
     g.ld_add = d;
-    g.dual_rows = c.use_cfg ? BN : 0;
+    g.dual_rows = ns == 2 * c.B ? BN : 0;
     KCK(gemm(bf, EPI_INPROJ, g, st));
     ConvArgs cv{};
-    cv.S = c.S;
+    cv.S = ns;
     cv.L = c.N;
     cv.d = d;
     cv.rowkeep = dit ? keep : nullptr;  // UNetT's InputEmbedding passes no mask (unett.py:100)
-    cv.x = b.h0;
+    cv.x = b.h0 + no * d;
     cv.x_f32 = 1;
     cv.w = e->conv_w[0];
     cv.bias = e->conv_b[0];
     cv.mode = 0;
-    cv.y = b.c1;
+    cv.y = op(b.c1, no, d);
     {
       ProbeScope ps(e, KC_CONV, st, &c.site);
       KCK(conv_pos(bf, cv, st));
     }
-    cv.x = b.c1;
+    cv.x = op(b.c1, no, d);
     cv.x_f32 = bf ? 0 : 1;
     cv.w = e->conv_w[1];
     cv.bias = e->conv_b[1];
     cv.mode = 1;
-    cv.y = b.h;
+    cv.y = bh;
     cv.y_seq_stride = c.L;
     cv.y_row_off = dit ? 0 : 1;
-    cv.resid = b.h0;
+    cv.resid = b.h0 + no * d;
     KCK(conv_pos(bf, cv, st));
   }
-  if (!dit) KCK(write_time_token(b.temb_cur, c.S, c.L, d, b.h, st));
+  if (!dit) KCK(write_time_token(b.temb_cur, ns, c.L, d, bh, st));
 
   const float* ada_k = dit ? b.ada_cur : nullptr;
-  float* h = b.h;
-  float* h2 = b.h2;
+  float* h = bh;
+  float* h2 = bh2;
   for (int l = 0; l < a.depth; ++l) {
     Layer& Ly = e->layers[l];
     const float* ad = ada_k ? ada_k + (size_t)l * 6 * d : nullptr;
     if (!dit) {
       if (l < a.depth / 2) {
         // skips are only ever GEMM A operands: keep them in the operand dtype
-        KCK(f32_to_op(bf, h, (int64_t)rows * d, b.skips[l], st));
+        KCK(f32_to_op(bf, h, (int64_t)rows * d, op(b.skips[l], ro, d), st));
       } else {
         // skip_proj(cat(x, skip)) = x.W1^T + skip.W2^T (unett.py:288-297)
-        KCK(f32_to_op(bf, h, (int64_t)rows * d, b.aop, st));
-        GemmArgs g = gargs(b.aop, d, Ly.skip1, rows, h2, d);
+        KCK(f32_to_op(bf, h, (int64_t)rows * d, aop, st));
+        GemmArgs g = gargs(aop, d, Ly.skip1, rows, h2, d);
         KCK(gemm(bf, EPI_STORE, g, st));
-        g = gargs(b.skips[a.depth - 1 - l], d, Ly.skip2, rows, h2, d);
+        g = gargs(op(b.skips[a.depth - 1 - l], ro, d), d, Ly.skip2, rows, h2, d);
         KCK(gemm(bf, EPI_RESID, g, st));
         std::swap(h, h2);
       }
-      KCK(rms_norm_g(bf, h, rows, d, Ly.g_attn, b.aop, st));
+      KCK(rms_norm_g(bf, h, rows, d, Ly.g_attn, aop, st));
     } else {
-      KCK(ln_modulate(bf, h, rows, d, ad /*shift_msa*/, ad + d /*scale_msa*/, b.aop, st));
+      KCK(ln_modulate(bf, h, rows, d, ad /*shift_msa*/, ad + d /*scale_msa*/, aop, st));
     }
     {
-      GemmArgs g = gargs(b.aop, d, Ly.qkv, rows, nullptr, 0);
+      GemmArgs g = gargs(aop, d, Ly.qkv, rows, nullptr, 0);
       g.rope = b.rope;
       g.seq_len = c.L;
       g.heads = H;
       g.rope_heads = a.pe_attn_head > 0 ? a.pe_attn_head : H;
-      g.q = b.q;
-      g.k = b.k;
-      g.v = b.v;
+      g.q = q;
+      g.k = k;
+      g.v = v;
       g.q_scale = 0.125f * 1.4426950408889634f;  // softmax scale 1/sqrt(64) in log2 units, folded into q
       ProbeScope ps(e, KC_QKV, st, &c.site, &g.probe);
       KCK(gemm(bf, EPI_QKV, g, st));
     }
     {
       AttnArgs at{};
-      at.q = b.q;
-      at.k = b.k;
-      at.v = b.v;
-      at.o = b.o;
-      at.S = c.S;
+      at.q = q;
+      at.k = k;
+      at.v = v;
+      at.o = o;
+      at.S = ns;
       at.H = H;
       at.L = c.L;
-      at.kv_len = (a.attn_mask_enabled && c.batch_mask) ? b.kvlen : nullptr;
+      at.kv_len = (a.attn_mask_enabled && c.batch_mask) ? b.kvlen + s0 : nullptr;
       at.scale = 0.125f;
       at.prescaled = 1;
       ProbeScope ps(e, KC_ATTN, st, &c.site, &at.probe);
       KCK(attention(bf, at, st));
     }
     {
-      GemmArgs g = gargs(b.o, inner, Ly.out, rows, h, d);
+      GemmArgs g = gargs(o, inner, Ly.out, rows, h, d);
       g.gate = ad ? ad + 2 * d : nullptr;  // gate_msa
       g.rowkeep = keep;                    // masked_fill of pad rows (modules.py:552-554)
       ProbeScope ps(e, KC_OUT, st, &c.site, &g.probe);
@@ -702,17 +725,17 @@ static int backbone_step(Ctx& c) {
     {
       ProbeScope ps(e, KC_NORM, st, &c.site);
       if (dit)
-        KCK(ln_modulate(bf, h, rows, d, ad + 3 * d /*shift_mlp*/, ad + 4 * d /*scale_mlp*/, b.aop, st));
+        KCK(ln_modulate(bf, h, rows, d, ad + 3 * d /*shift_mlp*/, ad + 4 * d /*scale_mlp*/, aop, st));
       else
-        KCK(rms_norm_g(bf, h, rows, d, Ly.g_ff, b.aop, st));
+        KCK(rms_norm_g(bf, h, rows, d, Ly.g_ff, aop, st));
     }
     {
-      GemmArgs g = gargs(b.aop, d, Ly.ff1, rows, b.f, a.ff_dim);
+      GemmArgs g = gargs(aop, d, Ly.ff1, rows, f, a.ff_dim);
       ProbeScope ps(e, KC_FFN1, st, &c.site, &g.probe);
       KCK(gemm(bf, EPI_GELU_TANH, g, st));
     }
     {
-      GemmArgs g = gargs(b.f, a.ff_dim, Ly.ff2, rows, h, d);
+      GemmArgs g = gargs(f, a.ff_dim, Ly.ff2, rows, h, d);
       g.gate = ad ? ad + 5 * d : nullptr;  // gate_mlp
       ProbeScope ps(e, KC_FFN2, st, &c.site, &g.probe);
       KCK(gemm(bf, EPI_RESID, g, st));
@@ -720,12 +743,28 @@ static int backbone_step(Ctx& c) {
   }
   if (dit) {
     const float* fin = ada_k + (size_t)a.depth * 6 * d;  // AdaLayerNorm_Final: (scale, shift)
-    KCK(ln_modulate(bf, h, rows, d, fin + d, fin, b.aop, st));
+    KCK(ln_modulate(bf, h, rows, d, fin + d, fin, aop, st));
   } else {
-    KCK(rms_norm_g(bf, h, rows, d, e->norm_out_g, b.aop, st));
+    KCK(rms_norm_g(bf, h, rows, d, e->norm_out_g, aop, st));
   }
-  GemmArgs g = gargs(b.aop, d, e->proj_out, rows, b.p, a.mel_dim);
+  GemmArgs g = gargs(aop, d, e->proj_out, rows, b.p + ro * a.mel_dim, a.mel_dim);
   KCK(gemm(bf, EPI_STORE, g, st));
+  return 0;
+}
+
+// One packed cond/uncond backbone forward for the current step; result in b.p [S, L, mel]. With a
+// second stream (c.st2, graph capture only) the conditional and unconditional branches run as two
+// independent launch chains (fork/join by events), so one chain's kernel heads and tails overlap
+// the other's bodies instead of leaving CUs idle at every kernel boundary.
+static int backbone_step(Ctx& c) {
+  if (!c.st2 || !c.use_cfg) return backbone_part(c, 0, c.S, c.st);
+  f5h_engine* e = c.e;
+  KCK(hipEventRecord(e->ev_fork, c.st));
+  KCK(hipStreamWaitEvent(c.st2, e->ev_fork, 0));
+  RC(backbone_part(c, 0, c.B, c.st));
+  RC(backbone_part(c, c.B, c.B, c.st2));
+  KCK(hipEventRecord(e->ev_join, c.st2));
+  KCK(hipStreamWaitEvent(c.st, e->ev_join, 0));
   return 0;
 }
 
@@ -764,6 +803,7 @@ int f5h_engine_create(const f5h_arch* arch, const f5h_weight* weights, int32_t n
   e->esz = e->bf ? 2 : 4;
   e->tdp = (arch->text_dim + 63) / 64 * 64;
   if (const char* gv = getenv("F5H_GRAPH")) e->graph_mode = atoi(gv) ? 1 : 0;
+  if (const char* sv = getenv("F5H_SPLIT_CFG")) e->split_cfg = std::min(2, std::max(0, atoi(sv)));
   WMap W;
   for (int i = 0; i < n_weights; ++i) W.m[weights[i].name] = {weights[i].data, weights[i].numel};
   int rc = pack_all(e, W);
@@ -793,6 +833,9 @@ void f5h_engine_destroy(f5h_engine* e) {
   if (!e) return;
   e->graphs.clear();
   if (e->cap) (void)hipStreamDestroy(e->cap);
+  if (e->cap2) (void)hipStreamDestroy(e->cap2);
+  if (e->ev_fork) (void)hipEventDestroy(e->ev_fork);
+  if (e->ev_join) (void)hipEventDestroy(e->ev_join);
   for (void* p : e->allocs) (void)hipFree(p);
   delete e;
 }
@@ -901,6 +944,8 @@ static int run_steps(Ctx& c, const f5h_sample_args* a, const void* ws) {
   key.use_cfg = c.use_cfg;
   key.batch_mask = c.batch_mask;
   key.probe = e->probe_class;
+  const bool split = e->split_cfg == 1 || (e->split_cfg == 2 && c.B >= 4);
+  key.split = split;
   key.kernel_epoch = g_kernel_epoch.load();
   std::memcpy(&key.cfg_bits, &a->cfg_strength, 4);
   std::shared_ptr<GraphEntry> hold;  // keeps the replayed graph alive through the launch loop
@@ -910,10 +955,16 @@ static int run_steps(Ctx& c, const f5h_sample_args* a, const void* ws) {
       if (x->key == key) hold = x;
     if (!hold) {
       if (!e->cap) HIPCK(hipStreamCreateWithFlags(&e->cap, hipStreamNonBlocking));
+      if (split && !e->cap2) {
+        HIPCK(hipStreamCreateWithFlags(&e->cap2, hipStreamNonBlocking));
+        HIPCK(hipEventCreateWithFlags(&e->ev_fork, hipEventDisableTiming));
+        HIPCK(hipEventCreateWithFlags(&e->ev_join, hipEventDisableTiming));
+      }
       auto ne = std::make_shared<GraphEntry>();
       ne->key = key;
       Ctx cc = c;
       cc.st = e->cap;
+      cc.st2 = split ? e->cap2 : nullptr;
       hipError_t be = hipStreamBeginCapture(e->cap, hipStreamCaptureModeThreadLocal);
       if (be != hipSuccess) return fail(F5H_EHIP, std::string("hipStreamBeginCapture: ") + hipGetErrorString(be));
       const int rc = enqueue_step(cc, a);
@@ -1031,6 +1082,14 @@ int f5h_set_graph_mode(f5h_engine* e, int32_t mode) {
   return 0;
 }
 
+int f5h_set_cfg_streams(f5h_engine* e, int32_t n) {
+  if (!e) return fail(F5H_EINVAL, "null engine");
+  if (n < 0 || n > 2) return fail(F5H_EINVAL, "cfg streams must be 0 (auto), 1 or 2");
+  std::lock_guard<std::mutex> g(e->gm);
+  e->split_cfg = n == 0 ? 2 : (n == 2 ? 1 : 0);
+  return 0;
+}
+
 int f5h_graph_stats(f5h_engine* e, int64_t* captures, int64_t* replays, int32_t* cached) {
   if (!e) return fail(F5H_EINVAL, "null engine");
   std::lock_guard<std::mutex> g(e->gm);
@@ -1075,8 +1134,8 @@ int f5h_op_linear(void* stream, int32_t compute, int32_t M, int32_t N, int32_t K
 }
 
 int f5h_gemm_force_config(int32_t cfg) {
-  if (cfg != -1 && cfg != 0 && cfg != 1 && cfg != 5 && cfg != 11)
-    return fail(F5H_EINVAL, "gemm config must be -1, 0, 1, 5 or 11");
+  if (cfg < -1 || cfg > 24 || cfg == 10 || cfg == 13 || cfg == 15 || (cfg > 16 && cfg < 20))
+    return fail(F5H_EINVAL, "gemm config must be -1, 0..9, 11, 12, 14, 16 or 20..24");
   gemm_force_config(cfg);
   g_kernel_epoch.fetch_add(1);
   return 0;

@@ -1,0 +1,844 @@
+// MFMA GEMM with fused epilogues: C[M,N] = A[M,K] . W[N,K]^T (+ epilogue).
+//
+// Every nn.Linear on the CFM hot path lands here: QKV + RoPE
+// (modules.py:481-509), out-proj + gated residual (modules.py:548-554,751), FFN1 + GELU-tanh
+// and FFN2 + gated residual (modules.py:359-361,754-755), the hoisted input projection
+// (dit.py:162), proj_out (dit.py:368), the all-steps AdaLN table (modules.py:321-323) and
+// the ConvNeXt pointwise convs (modules.py:265-269).
+//
+// Main loop: 256 threads = 4 waves as 2x2, block tile BM x 128 (BM = 128, or 64 when the
+// 128-row grid would leave CUs without a second block), K staged 128 bytes per row per
+// stage (64 bf16 / 32 fp32) by LDS-DMA (global_load_lds) into a double-buffered,
+// XOR-swizzled LDS image; A and W are both K-contiguous operand-dtype panels, so every
+// fragment is one ds_read_b128. bf16 mode: v_mfma_f32_16x16x32_bf16; fp32 parity mode:
+// v_mfma_f32_16x16x4_f32 (exact f32).
+// Epilogue: the fp32 accumulator tile is staged through LDS (padded rows) and re-read
+// row-contiguously, so every global access of the epilogue (bias, gate, residual, RoPE
+// table, q/k/v scatter) is a 16-32 byte vector access on whole rows.
+//
+// This header holds the kernels and their launch templates; gemm.hip holds the host-side tile
+// choice and the dtype dispatcher, gemm_{bf16,f16,f32}*.hip instantiate the launchers (split so
+// that hipcc builds them in parallel).
+#pragma once
+#include "common.h"
+#include "kernels.h"
+
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+
+namespace f5h {
+
+// tile configuration for a 16-bit GEMM of this shape (forced, F5H_GEMM_CFG, F5H_GEMM_MAP, or pick_cfg)
+int gemm_select_cfg(const GemmArgs& a);
+
+
+// Block tile BM x BN with WGM x WGN waves; every wave owns a (BM/WGM) x (BN/WGN) sub-tile.
+// KB = bytes of K per row per LDS stage: 128 (64 bf16, two MFMA k-slabs per barrier) or 64 (32 bf16,
+// one slab: half the bytes per stage, so the same LDS holds a ring twice as deep).
+template <int BM, int BN, int WGM, int WGN, int NS, int KB = 128>
+struct GemmCfg {
+  static constexpr int NW = WGM * WGN, THREADS = 64 * NW;
+  static constexpr int WM = BM / WGM, WN = BN / WGN, MT = WM / 16, NT = WN / 16;
+  static constexpr int CPR = KB / 16;                        // 16-B chunks per row per stage
+  static constexpr int stage_bytes = (BM + BN) * KB;
+  static constexpr int main_bytes = NS * stage_bytes;
+  static constexpr int EPAD = WN + 4;                        // fp32 row of a wave's epilogue strip
+  static constexpr int epi_bytes = NW * 16 * EPAD * 4;       // one 16-row strip per wave
+  static constexpr int bytes = main_bytes > epi_bytes ? main_bytes : epi_bytes;
+  static_assert(KB == 128 || KB == 64, "stage row bytes");
+  static_assert(BM * CPR % THREADS == 0 && BN * CPR % THREADS == 0, "whole DMA rounds per stage");
+  static_assert(MT * 16 == WM && NT * 16 == WN && MT + NT <= 15, "fragment counts (lgkmcnt <= 15)");
+};
+
+// 64-byte rows (K32 stages): chunk c of row r sits at c ^ f[(r>>2)&3], f = {0,2,3,1}: conflict-free
+// for ds_read_b128, whose four 16-lane groups ({0-3,12-15,20-27}, ...) each read rows {r, r+12}
+// at chunk c and rows r+4..r+11 at chunk c+1.
+F5H_DEV int swz64(int row, int chunk) {
+  const int b = (row >> 2) & 3;
+  return chunk ^ ((0x1320 >> (4 * b)) & 3);  // f = {0,2,3,1}
+}
+
+// ds_read_b128 the compiler does not see (no waitcnt bookkeeping): the caller waits lgkmcnt itself
+template <int OFF>
+F5H_DEV u32x4 lds_read_b128(uint32_t addr) {
+  u32x4 r;
+  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(r) : "v"(addr), "i"(OFF));
+  return r;
+}
+
+// 8 consecutive fp32 values of one row
+struct V8 {
+  float v[8];
+};
+
+template <typename TC>
+F5H_DEV void store8(TC* p, const V8& x);
+template <>
+F5H_DEV void store8<float>(float* p, const V8& x) {
+  *reinterpret_cast<float4*>(p) = make_float4(x.v[0], x.v[1], x.v[2], x.v[3]);
+  *reinterpret_cast<float4*>(p + 4) = make_float4(x.v[4], x.v[5], x.v[6], x.v[7]);
+}
+template <>
+F5H_DEV void store8<bf16>(bf16* p, const V8& x) {
+  bf16x8 b = {f2bf(x.v[0]), f2bf(x.v[1]), f2bf(x.v[2]), f2bf(x.v[3]),
+              f2bf(x.v[4]), f2bf(x.v[5]), f2bf(x.v[6]), f2bf(x.v[7])};
+  *reinterpret_cast<bf16x8*>(p) = b;
+}
+template <>
+F5H_DEV void store8<f16>(f16* p, const V8& x) {
+  f16x8 b = {(f16)x.v[0], (f16)x.v[1], (f16)x.v[2], (f16)x.v[3], (f16)x.v[4], (f16)x.v[5], (f16)x.v[6], (f16)x.v[7]};
+  *reinterpret_cast<f16x8*>(p) = b;
+}
+F5H_DEV V8 load8(const float* p) {
+  float4 a = *reinterpret_cast<const float4*>(p), b = *reinterpret_cast<const float4*>(p + 4);
+  return V8{{a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w}};
+}
+
+// Epilogue arithmetic with explicit rounding (no FMA contraction), shared by every kernel so that
+// all tile configurations stay bitwise identical whatever the compiler contracts around them.
+F5H_DEV float rope_re(float a, float b, float c, float s) { return sub_nc(mul_nc(a, c), mul_nc(b, s)); }
+F5H_DEV float rope_im(float a, float b, float c, float s) { return add_nc(mul_nc(b, c), mul_nc(a, s)); }
+F5H_DEV float resid_add(float c, float gate, float x, float keep) { return add_nc(c, mul_nc(gate, mul_nc(x, keep))); }
+
+// n / d for 0 <= n < 2^24, d > 0: float quotient + one-step correction (no integer division loop)
+F5H_DEV int fdiv(int n, int d) {
+  int q = (int)((float)n * __builtin_amdgcn_rcpf((float)d));
+  q -= q * d > n;
+  q += (q + 1) * d <= n;
+  return q;
+}
+
+// Apply the epilogue to 8 consecutive columns [col, col+8) of output row `row`.
+template <typename TC, int EPI>
+F5H_DEV void epi8(const GemmArgs& g, int row, int col, V8 x, const V8* pre = nullptr) {
+  const bool full = col + 8 <= g.N;
+  if (g.bias) {
+    if (full) {
+      V8 b = load8(g.bias + col);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) x.v[e] = add_nc(x.v[e], b.v[e]);
+    } else {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) x.v[e] = add_nc(x.v[e], col + e < g.N ? g.bias[col + e] : 0.f);
+    }
+  }
+  if constexpr (EPI == EPI_QKV) {
+    // interleaved RoPE pairs (2i, 2i+1) (x_transformers rotate_half) never straddle an 8-column chunk;
+    // a 64-column head maps to one contiguous 128 B row segment of q/k/v [S,H,L,64]
+    const int inner = g.heads * 64;
+    const int which = fdiv(col, inner), hc = col - which * inner;
+    const int head = hc >> 6, dh = hc & 63;
+    const int s = fdiv(row, g.seq_len), pos = row - s * g.seq_len;
+    if (which < 2 && head < g.rope_heads) {
+      const float4* cs = reinterpret_cast<const float4*>(g.rope + (int64_t)pos * 32 + (dh >> 1));
+#pragma unroll
+      for (int pr = 0; pr < 2; ++pr) {
+        float4 c2 = cs[pr];  // (cos, sin) of two consecutive pairs
+        float a0 = x.v[4 * pr + 0], a1 = x.v[4 * pr + 1], b0 = x.v[4 * pr + 2], b1 = x.v[4 * pr + 3];
+        x.v[4 * pr + 0] = rope_re(a0, a1, c2.x, c2.y);
+        x.v[4 * pr + 1] = rope_im(a0, a1, c2.x, c2.y);
+        x.v[4 * pr + 2] = rope_re(b0, b1, c2.z, c2.w);
+        x.v[4 * pr + 3] = rope_im(b0, b1, c2.z, c2.w);
+      }
+    }
+    if (which == 0 && g.q_scale != 0.f && g.q_scale != 1.f) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) x.v[e] = mul_nc(x.v[e], g.q_scale);
+    }
+    TC* dst = reinterpret_cast<TC*>(which == 0 ? g.q : (which == 1 ? g.k : g.v));
+    store8<TC>(dst + (((int64_t)s * g.heads + head) * g.seq_len + pos) * 64 + dh, x);
+    return;
+  }
+  const int64_t off = (int64_t)row * g.ldc + col;
+  const bool vec = full && (g.ldc % 4 == 0);
+  if constexpr (EPI == EPI_GELU_TANH || EPI == EPI_GELU_ERF_OP) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e)
+      x.v[e] = EPI == EPI_GELU_ERF_OP ? gelu_erf(x.v[e])
+                                      : (is16<TC>() ? gelu_tanh_fast(x.v[e]) : gelu_tanh(x.v[e]));
+    TC* C = reinterpret_cast<TC*>(g.C);
+    if (full && g.ldc % 8 == 0) {
+      store8<TC>(C + off, x);
+    } else {
+      for (int e = 0; e < 8; ++e)
+        if (col + e < g.N) C[off + e] = from_f32<TC>(x.v[e]);
+    }
+    return;
+  } else {
+    float* C = reinterpret_cast<float*>(g.C);
+    if constexpr (EPI == EPI_SILU) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) x.v[e] = silu(x.v[e]);
+    } else if constexpr (EPI == EPI_GELU_ERF) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) x.v[e] = gelu_erf(x.v[e]);
+    } else if constexpr (EPI == EPI_RESID) {
+      const float keep = (g.rowkeep && !g.rowkeep[row]) ? 0.f : 1.f;
+      V8 c = vec ? (pre ? *pre : load8(C + off)) : V8{};
+      if (!vec)
+        for (int e = 0; e < 8; ++e) c.v[e] = col + e < g.N ? C[off + e] : 0.f;
+      V8 gt = g.gate ? (full ? load8(g.gate + col) : V8{}) : V8{{1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f}};
+      if (g.gate && !full)
+        for (int e = 0; e < 8; ++e) gt.v[e] = col + e < g.N ? g.gate[col + e] : 0.f;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) x.v[e] = resid_add(c.v[e], gt.v[e], x.v[e], keep);
+    } else if constexpr (EPI == EPI_RESID_FILL) {
+      const bool keep = !g.rowkeep || g.rowkeep[row];
+      V8 c = vec ? load8(C + off) : V8{};
+      if (!vec)
+        for (int e = 0; e < 8; ++e) c.v[e] = col + e < g.N ? C[off + e] : 0.f;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) x.v[e] = keep ? c.v[e] + x.v[e] : 0.f;
+    } else if constexpr (EPI == EPI_INPROJ) {
+      const int64_t ao = (int64_t)row * g.ld_add + col;
+      V8 a0 = load8(g.add + ao);
+      V8 o0, o1;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) o0.v[e] = x.v[e] + a0.v[e];
+      store8<float>(C + off, o0);
+      if (g.dual_rows) {
+        V8 a1 = load8(g.add + ao + g.dual_rows * g.ld_add);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) o1.v[e] = x.v[e] + a1.v[e];
+        store8<float>(C + off + g.dual_rows * g.ldc, o1);
+      }
+      return;
+    }
+    if (vec) {
+      store8<float>(C + off, x);
+    } else {
+      for (int e = 0; e < 8; ++e)
+        if (col + e < g.N) C[off + e] = x.v[e];
+    }
+  }
+}
+
+// wait until at most `n` of this wave's VMEM ops (n/DPS stages) are outstanding
+template <int DPS>
+F5H_DEV void wait_stages(int n_stages) {
+  switch (n_stages) {
+    case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+    case 1: asm volatile("s_waitcnt vmcnt(%0)" ::"i"(DPS) : "memory"); break;
+    case 2: asm volatile("s_waitcnt vmcnt(%0)" ::"i"(2 * DPS) : "memory"); break;
+    case 3: asm volatile("s_waitcnt vmcnt(%0)" ::"i"(3 * DPS) : "memory"); break;
+    default: asm volatile("s_waitcnt vmcnt(%0)" ::"i"(4 * DPS) : "memory"); break;
+  }
+}
+
+// FAST: the launcher guarantees whole-column tiles (N % BN == 0, ldc % 8 == 0) for the hot
+// epilogues, so the epilogue is compiled without per-element column guards (see below).
+template <typename TC, int EPI, int BM, int BN, int WGM, int WGN, int NS, bool FAST = false, int KB = 128>
+__global__ __launch_bounds__(64 * WGM * WGN, 1) void gemm_kernel(GemmArgs g) {
+  const ProbeT probe_t = probe_enter(g.probe);
+  typedef GemmCfg<BM, BN, WGM, WGN, NS, KB> C;
+  constexpr int E = elems16<TC>();
+  constexpr int CPR = C::CPR, SLABS = KB / 64;
+  constexpr int BKE = CPR * E;
+  constexpr int NW = C::NW, WM = C::WM, WN = C::WN, MT = C::MT, NT = C::NT;
+  constexpr int AR = BM * CPR / C::THREADS, BR = BN * CPR / C::THREADS;  // DMA rounds per stage
+  constexpr int DPS = AR + BR;                                            // DMA instructions per stage per wave
+  static_assert(NS >= 2 && NS <= 6 && (NS - 1) * DPS <= 63, "LDS stages");  // NS-1 stages in flight
+  typedef typename Slab<TC>::frag frag;
+  auto swz = [](int row, int chunk) { return KB == 128 ? swz128(row, chunk) : swz64(row, chunk); };
+
+  __shared__ __attribute__((aligned(16))) uint4 lds[C::bytes / 16];
+  constexpr int stage_u4 = C::stage_bytes / 16;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid / WGN, wn = wid % WGN;
+  const int ntn = (g.N + BN - 1) / BN;
+  // XCD-aware remap (cdna_hip_programming.md T1, bijective form): blocks b and b+8 share an
+  // XCD, so give each XCD a contiguous run of n-fastest tiles -> its L2 holds whole A panels
+  const int nwg = gridDim.x, b = blockIdx.x, xq = nwg >> 3, xr = nwg & 7, xcd = b & 7;
+  const int bid = (xcd < xr ? xcd * (xq + 1) : xr * (xq + 1) + (xcd - xr) * xq) + (b >> 3);
+  const int m0 = (bid / ntn) * BM, n0 = (bid % ntn) * BN;
+  const TC* A = reinterpret_cast<const TC*>(g.A);
+  const TC* W = reinterpret_cast<const TC*>(g.W);
+
+  // per-lane DMA source offsets (elements), fixed across K-steps. The swizzle goes on the
+  // SOURCE chunk so that (wave-uniform LDS base + lane*16) lands on the swz128 image.
+  int64_t aoff[AR], boff[BR];
+  static_for<0, AR>([&](auto I) {
+    constexpr int i = decltype(I)::value;
+    const int p = (i * NW + wid) * 64 + lane, row = p / CPR, slot = p % CPR;
+    const int m = min(m0 + row, g.M - 1);  // rows past M feed only unstored outputs
+    aoff[i] = (int64_t)m * g.lda + swz(row, slot) * E;
+  });
+  static_for<0, BR>([&](auto I) {
+    constexpr int i = decltype(I)::value;
+    const int p = (i * NW + wid) * 64 + lane, row = p / CPR, slot = p % CPR;
+    const int n = min(n0 + row, g.N - 1);  // likewise for weight rows past N
+    boff[i] = (int64_t)n * g.ldw + swz(row, slot) * E;
+  });
+  auto stage = [&](int buf, int k0) {
+    uint4* As = lds + buf * stage_u4;
+    uint4* Bs = As + BM * CPR;
+    static_for<0, AR>([&](auto I) {
+      constexpr int i = decltype(I)::value;
+      __builtin_amdgcn_global_load_lds((const void*)(A + aoff[i] + k0), (LDS_PTR(void))(As + (i * NW + wid) * 64),
+                                       16, 0, 0);
+    });
+    static_for<0, BR>([&](auto I) {
+      constexpr int i = decltype(I)::value;
+      __builtin_amdgcn_global_load_lds((const void*)(W + boff[i] + k0), (LDS_PTR(void))(Bs + (i * NW + wid) * 64),
+                                       16, 0, 0);
+    });
+  };
+
+  // Fragment reads are inline-asm ds_read_b128 so that hipcc does not put a vmcnt(0) (for the
+  // LDS-DMA still in flight into the OTHER stages) in front of them; their completion is waited
+  // for by hand (lgkmcnt(0) + sched_barrier, cdna_hip_programming.md §5.7 form iii).
+  // Row r of a fragment has r & 15 == lane & 15 (swz128 reads row bits 1..3), so the swizzled
+  // chunk depends only on the lane:
+  // per slab one base address per lane, the 16-row tiles at immediate offsets i*2048.
+  const uint32_t lds0 = (uint32_t)(uintptr_t)(LDS_PTR(void))lds;
+  const int fr = lane & 15, q = lane >> 4;
+  uint32_t abase[SLABS], bbase[SLABS];
+#pragma unroll
+  for (int s = 0; s < SLABS; ++s) {
+    abase[s] = lds0 + (wm * WM + fr) * KB + swz(fr, s * 4 + q) * 16;
+    bbase[s] = lds0 + BM * KB + (wn * WN + fr) * KB + swz(fr, s * 4 + q) * 16;
+  }
+
+  f32x4 acc[MT][NT];
+#pragma unroll
+  for (int i = 0; i < MT; ++i)
+#pragma unroll
+    for (int j = 0; j < NT; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // EPI_RESID: the residual rows this lane's epilogue reads are fetched before the K loop (the
+  // oldest VMEM ops, retired by the first stage wait), so the epilogue's read-modify-write does
+  // not expose a dependent HBM/MALL round trip. Register budget: small tiles only.
+  constexpr int CH_ = WN / 8, TPS = 16 * CH_ / 64;
+  constexpr bool PREF = EPI == EPI_RESID && is16<TC>() && (16 * CH_) % 64 == 0 &&
+                        MT * TPS * 8 <= 32;
+  V8 pre[PREF ? MT : 1][PREF ? TPS : 1];
+  if constexpr (PREF) {
+    const float* Cp = reinterpret_cast<const float*>(g.C);
+    const int fr_ = lane & 15, q_ = lane >> 4;
+    (void)fr_;
+    (void)q_;
+#pragma unroll
+    for (int i = 0; i < MT; ++i)
+#pragma unroll
+      for (int t = 0; t < TPS; ++t) {
+        const int idx = t * 64 + lane, rr = idx / CH_, cc = idx % CH_;
+        const int row = m0 + wm * WM + i * 16 + rr, col = n0 + wn * WN + cc * 8;
+        const bool ok = row < g.M && col + 8 <= g.N && g.ldc % 4 == 0;
+        pre[i][t] = ok ? load8(Cp + (int64_t)row * g.ldc + col) : V8{};
+      }
+  }
+
+  const int nk = g.K / BKE;
+  for (int p = 0; p < NS - 1 && p < nk; ++p) stage(p, p * BKE);
+  for (int kt = 0; kt < nk; ++kt) {
+    // stage kt has landed for THIS wave once at most the younger in-flight stages remain;
+    // the barrier then publishes every wave's part of it
+    wait_stages<DPS>(min(NS - 2, nk - 1 - kt));
+    __builtin_amdgcn_s_barrier();
+    const uint32_t soff = (uint32_t)((kt % NS) * C::stage_bytes);
+    u32x4 ar[SLABS][MT], br[SLABS][NT];
+#pragma unroll
+    for (int s = 0; s < SLABS; ++s) {
+      static_for<0, MT>([&](auto I) {
+        constexpr int i = decltype(I)::value;
+        ar[s][i] = lds_read_b128<i * 16 * KB>(abase[s] + soff);
+      });
+      static_for<0, NT>([&](auto J) {
+        constexpr int j = decltype(J)::value;
+        br[s][j] = lds_read_b128<j * 16 * KB>(bbase[s] + soff);
+      });
+    }
+    // WAR: slot (kt+NS-1)%NS == (kt-1)%NS was last read in iteration kt-1, whose reads all
+    // completed before that iteration's MFMAs, i.e. before every wave reached this barrier
+    if (kt + NS - 1 < nk) stage((kt + NS - 1) % NS, (kt + NS - 1) * BKE);
+    if constexpr (SLABS == 1) {
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+      for (int i = 0; i < MT; ++i) asm volatile("" : "+v"(ar[0][i]));
+#pragma unroll
+      for (int j = 0; j < NT; ++j) asm volatile("" : "+v"(br[0][j]));
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int i = 0; i < MT; ++i)
+#pragma unroll
+        for (int j = 0; j < NT; ++j)
+          acc[i][j] = Slab<TC>::mma(__builtin_bit_cast(frag, ar[0][i]), __builtin_bit_cast(frag, br[0][j]), acc[i][j]);
+      continue;
+    } else {
+    // slab 0's reads are the oldest MT+NT LDS ops: consume them while slab 1's land
+    asm volatile("s_waitcnt lgkmcnt(%0)" ::"i"(MT + NT) : "memory");
+#pragma unroll
+    for (int i = 0; i < MT; ++i) asm volatile("" : "+v"(ar[0][i]));
+#pragma unroll
+    for (int j = 0; j < NT; ++j) asm volatile("" : "+v"(br[0][j]));
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int i = 0; i < MT; ++i)
+#pragma unroll
+      for (int j = 0; j < NT; ++j)
+        acc[i][j] = Slab<TC>::mma(__builtin_bit_cast(frag, ar[0][i]), __builtin_bit_cast(frag, br[0][j]), acc[i][j]);
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+    for (int i = 0; i < MT; ++i) asm volatile("" : "+v"(ar[1][i]));
+#pragma unroll
+    for (int j = 0; j < NT; ++j) asm volatile("" : "+v"(br[1][j]));
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int i = 0; i < MT; ++i)
+#pragma unroll
+      for (int j = 0; j < NT; ++j)
+        acc[i][j] = Slab<TC>::mma(__builtin_bit_cast(frag, ar[SLABS - 1][i]), __builtin_bit_cast(frag, br[SLABS - 1][j]),
+                                  acc[i][j]);
+    }
+  }
+  __syncthreads();
+
+  // ---- epilogue, per wave and 16-row strip: accumulators -> the wave's LDS strip (fp32,
+  // padded rows) -> 8-column chunks of whole rows, so the epilogue's global accesses are
+  // 16-32 B vectors along rows. Strips are wave-private: LDS order within a wave suffices.
+  float* Cs = reinterpret_cast<float*>(lds) + wid * 16 * C::EPAD;
+  constexpr int CH = WN / 8;  // 8-column chunks per strip row
+  constexpr int TPC = 16 * CH / 64;  // chunks per lane per strip
+  // Fast path (whole-column tiles of the hot epilogues): a lane's column chunk is the same in
+  // every strip, so bias/gate/QKV head indices are loaded once, and the row data of strip i+1
+  // (RoPE pairs, residual rows, row masks) is fetched before strip i stores: no vmcnt wait in
+  // the strip loop covers an older store (one strip of global round trips instead of one per
+  // chunk; measured 9.5 us of a 30.6 us QKV launch before).
+  constexpr bool FAST_EPI = FAST && (64 % CH == 0) && (16 * CH) % 64 == 0;
+  if constexpr (FAST_EPI) {
+    {
+      const int cc = lane % CH;
+      const int col = n0 + wn * WN + cc * 8;
+      V8 bias8 = g.bias ? load8(g.bias + col) : V8{};
+      V8 gate8 = V8{{1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f}};
+      if constexpr (EPI == EPI_RESID)
+        if (g.gate) gate8 = load8(g.gate + col);
+      int which = 0, head = 0, dh = 0;
+      bool rope_on = false;
+      float qsc = 1.f;
+      TC* qkv_dst = nullptr;
+      if constexpr (EPI == EPI_QKV) {
+        const int inner = g.heads * 64;
+        which = fdiv(col, inner);
+        const int hc = col - which * inner;
+        head = hc >> 6;
+        dh = hc & 63;
+        rope_on = which < 2 && head < g.rope_heads;
+        qsc = (which == 0 && g.q_scale != 0.f) ? g.q_scale : 1.f;
+        qkv_dst = reinterpret_cast<TC*>(which == 0 ? g.q : (which == 1 ? g.k : g.v));
+      }
+      struct RowIn {
+        V8 d;         // RoPE (cos, sin) of two pairs (QKV) or the residual row chunk (RESID)
+        float keep;   // RESID row mask
+      };
+      auto fetch = [&](int i, RowIn (&ri)[TPC]) {
+#pragma unroll
+        for (int t = 0; t < TPC; ++t) {
+          const int rr = t * (64 / CH) + lane / CH;
+          const int row = m0 + wm * WM + i * 16 + rr;
+          const bool ok = row < g.M;
+          ri[t].keep = 1.f;
+          if constexpr (EPI == EPI_QKV) {
+            ri[t].d = V8{};
+            if (ok && rope_on) {
+              const int pos = row - fdiv(row, g.seq_len) * g.seq_len;
+              ri[t].d = load8(reinterpret_cast<const float*>(g.rope + (int64_t)pos * 32 + (dh >> 1)));
+            }
+          } else if constexpr (EPI == EPI_RESID) {
+            if constexpr (PREF) {
+              ri[t].d = V8{};
+            } else {
+              ri[t].d = ok ? load8(reinterpret_cast<const float*>(g.C) + (int64_t)row * g.ldc + col) : V8{};
+            }
+            if (ok && g.rowkeep && !g.rowkeep[row]) ri[t].keep = 0.f;
+          } else {
+            ri[t].d = V8{};
+          }
+        }
+      };
+      RowIn rbuf[2][TPC];
+      fetch(0, rbuf[0]);
+      static_for<0, MT>([&](auto I) {
+        constexpr int i = decltype(I)::value;
+        if constexpr (i + 1 < MT) fetch(i + 1, rbuf[(i + 1) & 1]);
+#pragma unroll
+        for (int j = 0; j < NT; ++j)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) Cs[(q * 4 + r) * C::EPAD + j * 16 + fr] = acc[i][j][r];
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+        for (int t = 0; t < TPC; ++t) {
+          const int rr = t * (64 / CH) + lane / CH;
+          const int row = m0 + wm * WM + i * 16 + rr;
+          const float* src = Cs + rr * C::EPAD + cc * 8;
+          const float4 a0 = *reinterpret_cast<const float4*>(src), a1 = *reinterpret_cast<const float4*>(src + 4);
+          V8 x{{a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w}};
+          if (g.bias) {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) x.v[e] = add_nc(x.v[e], bias8.v[e]);
+          }
+          const RowIn& ri = rbuf[i & 1][t];
+          if (row < g.M) {
+            if constexpr (EPI == EPI_QKV) {
+              if (rope_on) {
+#pragma unroll
+                for (int pr = 0; pr < 2; ++pr) {
+                  const float c0 = ri.d.v[4 * pr + 0], s0 = ri.d.v[4 * pr + 1];
+                  const float c1 = ri.d.v[4 * pr + 2], s1 = ri.d.v[4 * pr + 3];
+                  const float a0_ = x.v[4 * pr + 0], a1_ = x.v[4 * pr + 1], b0 = x.v[4 * pr + 2], b1 = x.v[4 * pr + 3];
+                  x.v[4 * pr + 0] = rope_re(a0_, a1_, c0, s0);
+                  x.v[4 * pr + 1] = rope_im(a0_, a1_, c0, s0);
+                  x.v[4 * pr + 2] = rope_re(b0, b1, c1, s1);
+                  x.v[4 * pr + 3] = rope_im(b0, b1, c1, s1);
+                }
+              }
+              if (qsc != 1.f) {
+#pragma unroll
+                for (int e = 0; e < 8; ++e) x.v[e] = mul_nc(x.v[e], qsc);
+              }
+              const int sq = fdiv(row, g.seq_len), pos = row - sq * g.seq_len;
+              store8<TC>(qkv_dst + (((int64_t)sq * g.heads + head) * g.seq_len + pos) * 64 + dh, x);
+            } else if constexpr (EPI == EPI_RESID) {
+              const V8& c = PREF ? pre[PREF ? i : 0][PREF ? t : 0] : ri.d;
+              V8 o;
+#pragma unroll
+              for (int e = 0; e < 8; ++e) o.v[e] = resid_add(c.v[e], gate8.v[e], x.v[e], ri.keep);
+              store8<float>(reinterpret_cast<float*>(g.C) + (int64_t)row * g.ldc + col, o);
+            } else if constexpr (EPI == EPI_GELU_TANH || EPI == EPI_GELU_ERF_OP) {
+#pragma unroll
+              for (int e = 0; e < 8; ++e)
+                x.v[e] = EPI == EPI_GELU_ERF_OP ? gelu_erf(x.v[e])
+                                                : (is16<TC>() ? gelu_tanh_fast(x.v[e]) : gelu_tanh(x.v[e]));
+              store8<TC>(reinterpret_cast<TC*>(g.C) + (int64_t)row * g.ldc + col, x);
+            } else {  // EPI_STORE
+              store8<float>(reinterpret_cast<float*>(g.C) + (int64_t)row * g.ldc + col, x);
+            }
+          }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      });
+    }
+  }
+  if constexpr (!FAST_EPI) {
+#pragma unroll
+    for (int i = 0; i < MT; ++i) {
+#pragma unroll
+      for (int j = 0; j < NT; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) Cs[(q * 4 + r) * C::EPAD + j * 16 + fr] = acc[i][j][r];
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+      for (int t = 0; t < TPC; ++t) {
+        const int idx = t * 64 + lane, rr = idx / CH, cc = idx % CH;
+        const int row = m0 + wm * WM + i * 16 + rr, col = n0 + wn * WN + cc * 8;
+        const float* src = Cs + rr * C::EPAD + cc * 8;
+        float4 a = *reinterpret_cast<const float4*>(src), b = *reinterpret_cast<const float4*>(src + 4);
+        if (row < g.M && col < g.N)
+          epi8<TC, EPI>(g, row, col, V8{{a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w}}, PREF ? &pre[PREF ? i : 0][PREF ? t : 0] : nullptr);
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
+  }
+  probe_exit(g.probe, probe_t);
+}
+
+// ======================================================================================
+// Ping-pong GEMM (bf16 operands): 512 threads = two groups of 4 waves, one block per CU.
+// Group g owns output rows [g*BM/2, (g+1)*BM/2) of the BM x BN tile; its 4 waves split that
+// half as WGM2 x WGN2. The groups run half a period apart, so on every SIMD one wave issues
+// its MFMA cluster while its partner wave (other group) reads its next fragments from LDS and
+// issues LDS-DMA (MI355X_MICROARCH.md "Two waves per SIMD"):
+//
+//   half-period h:  2p       2p+1     2p+2  ...
+//   group 0:        mem(p)   mma(p)   mem(p+1)
+//   group 1:        mma(p-1) mem(p)   mma(p)
+//
+// with one s_barrier between half-periods. A phase p covers KS K32-stages. The LDS ring holds
+// R = D + 1 = 3 phases; phase p+2 is fetched during mem(p): group 0 brings its A rows, group 1
+// its B rows (so the vmcnt counts are group constants). Visibility of phase p+1 for the
+// readers of the next half-period: each issuing wave waits for its own DMA with a counted
+// vmcnt before the barrier that ends its mem phase (one phase younger stays in flight).
+// Slot reuse: phase p+2's slot held phase p-1, last read at half-period 2p-1 (group 1) and
+// retired (lgkmcnt(0)) before the barrier that ended it.
+//
+// LDS image of a stage: A rows [0,BM) then W rows [0,BN), 64 bytes (K32) per row = 4 chunks of
+// 16 B; chunk c of row r sits at c ^ f[(r>>2)&3], f = {0,2,3,1}: conflict-free for
+// ds_read_b128, whose four 16-lane groups ({0-3,12-15,20-27}, ...) each read rows
+// {r, r+12} at chunk c and rows r+4..r+11 at chunk c+1.
+// ======================================================================================
+template <int BM, int BN, int WGM2, int WGN2, int KS, int D>
+struct PPCfg {
+  static constexpr int WM = BM / 2 / WGM2, WN = BN / WGN2, MT = WM / 16, NT = WN / 16;
+  static constexpr int stage_bytes = (BM + BN) * 64;
+  static constexpr int R = D + 1;                              // ring phases
+  static constexpr int ring_bytes = R * KS * stage_bytes;
+  static constexpr int EPAD = WN + 4;
+  static constexpr int epi_bytes = 8 * 16 * EPAD * 4;
+  static constexpr int bytes = ring_bytes > epi_bytes ? ring_bytes : epi_bytes;
+  static constexpr int NA = BM / 64, NB = BN / 64;             // glds per stage per thread of a group
+  static_assert(WGM2 * WGN2 == 4, "4 waves per group");
+  static_assert(MT * 16 == WM && NT * 16 == WN, "16x16 fragments");
+  static_assert(NA * 64 == BM && NB * 64 == BN, "whole DMA rounds");
+  static_assert(bytes <= 160 * 1024, "LDS");
+};
+
+template <typename TC, int EPI, int BM, int BN, int WGM2, int WGN2, int KS, int D>
+__global__ __launch_bounds__(512, 1) void gemm_pp_kernel(GemmArgs g) {
+  const ProbeT probe_t = probe_enter(g.probe);
+  typedef PPCfg<BM, BN, WGM2, WGN2, KS, D> C;
+  constexpr int WM = C::WM, WN = C::WN, MT = C::MT, NT = C::NT, NA = C::NA, NB = C::NB;
+  constexpr int SB = C::stage_bytes, PB = KS * SB;  // stage / phase bytes
+  __shared__ __attribute__((aligned(16))) uint4 lds[C::bytes / 16];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int grp = wid >> 2, w4 = wid & 3;
+  const int wm = w4 / WGN2, wn = w4 % WGN2;
+  const int ntn = (g.N + BN - 1) / BN;
+  const int nwg = gridDim.x, b = blockIdx.x, xq = nwg >> 3, xr = nwg & 7, xcd = b & 7;
+  const int bid = (xcd < xr ? xcd * (xq + 1) : xr * (xq + 1) + (xcd - xr) * xq) + (b >> 3);
+  const int m0 = (bid / ntn) * BM, n0 = (bid % ntn) * BN;
+  const TC* A = reinterpret_cast<const TC*>(g.A);
+  const TC* W = reinterpret_cast<const TC*>(g.W);
+
+  // ---- DMA: group 0 stages the A rows, group 1 the W rows. Instruction i of wave w4 covers
+  // rows (i*4 + w4)*16 .. +15 of its operand; lane -> (row = lane>>2, physical chunk lane&3).
+  constexpr int NI = NA > NB ? NA : NB;
+  const int nI = grp == 0 ? NA : NB;
+  const TC* src[NI];
+  uint32_t dst_off[NI];
+#pragma unroll
+  for (int i = 0; i < NI; ++i) {
+    const int row = (i * 4 + w4) * 16 + (lane >> 2);
+    const int lc = swz64(row, lane & 3);  // logical chunk held at this physical slot
+    if (grp == 0) {
+      src[i] = A + (int64_t)min(m0 + row, g.M - 1) * g.lda + lc * 8;
+      dst_off[i] = (uint32_t)((i * 4 + w4) * 16 * 64);
+    } else {
+      src[i] = W + (int64_t)min(n0 + row, g.N - 1) * g.ldw + lc * 8;
+      dst_off[i] = (uint32_t)(BM * 64 + (i * 4 + w4) * 16 * 64);
+    }
+  }
+  char* lds_c = reinterpret_cast<char*>(lds);
+  auto dma_phase = [&](int p) {  // this wave's part of phase p (KS stages)
+    const int slot = p % C::R;
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+      const int k0 = (p * KS + s) * 32;
+#pragma unroll
+      for (int i = 0; i < NI; ++i)
+        if (i < nI)
+          __builtin_amdgcn_global_load_lds((const void*)(src[i] + k0),
+                                           (LDS_PTR(void))(lds_c + slot * PB + s * SB + dst_off[i]), 16, 0, 0);
+    }
+  };
+  // own DMA of phase `need` landed, given phases up to `issued` were issued (counted vmcnt:
+  // the younger phases stay in flight)
+  auto wait_dma = [&](int need, int issued) {
+    const int younger = min(max(issued - need, 0), D - 1);
+    static_for<0, D>([&](auto Y) {
+      constexpr int y = decltype(Y)::value;
+      if (younger == y) {
+        if (grp == 0)
+          asm volatile("s_waitcnt vmcnt(%0)" ::"i"(y * KS * NA) : "memory");
+        else
+          asm volatile("s_waitcnt vmcnt(%0)" ::"i"(y * KS * NB) : "memory");
+      }
+    });
+  };
+
+  // ---- fragment read addresses: row bits (r>>2)&3 are lane constants (tile bases are
+  // multiples of 16), so one base per operand per ring slot, tiles at immediate offsets
+  const uint32_t lds0 = (uint32_t)(uintptr_t)(LDS_PTR(void))lds;
+  const int fr = lane & 15, q = lane >> 4;
+  const int arow = grp * (BM / 2) + wm * WM + fr, brow = wn * WN + fr;
+  const uint32_t a_lane = lds0 + arow * 64 + swz64(arow, q) * 16;
+  const uint32_t b_lane = lds0 + BM * 64 + brow * 64 + swz64(brow, q) * 16;
+
+  f32x4 acc[MT][NT];
+#pragma unroll
+  for (int i = 0; i < MT; ++i)
+#pragma unroll
+    for (int j = 0; j < NT; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  u32x4 af[KS][MT], bfr[KS][NT];
+  auto read_phase = [&](int p) {
+    const uint32_t so = (uint32_t)((p % C::R) * PB);
+    static_for<0, KS>([&](auto S) {
+      constexpr int s = decltype(S)::value;
+      static_for<0, MT>([&](auto I) {
+        constexpr int i = decltype(I)::value;
+        af[s][i] = lds_read_b128<s * SB + i * 1024>(a_lane + so);
+      });
+      static_for<0, NT>([&](auto J) {
+        constexpr int j = decltype(J)::value;
+        bfr[s][j] = lds_read_b128<s * SB + j * 1024>(b_lane + so);
+      });
+    });
+  };
+
+  const int nph = g.K / (32 * KS);
+  for (int p = 0; p < D && p < nph; ++p) dma_phase(p);
+  wait_dma(0, min(D, nph) - 1);
+  __builtin_amdgcn_s_barrier();
+  if (grp == 1) __builtin_amdgcn_s_barrier();  // group 1 sits out half-period 0
+  for (int p = 0; p < nph; ++p) {
+    // ---- mem(p): fragments of phase p, DMA of phase p+2, wait for own part of phase p+1
+    read_phase(p);
+    if (p + D < nph) dma_phase(p + D);
+    wait_dma(p + 1, min(p + D, nph - 1));
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+#pragma unroll
+      for (int i = 0; i < MT; ++i) asm volatile("" : "+v"(af[s][i]));
+#pragma unroll
+      for (int j = 0; j < NT; ++j) asm volatile("" : "+v"(bfr[s][j]));
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    // ---- mma(p)
+    typedef typename Op16<TC>::v8 v8;
+#pragma unroll
+    for (int s = 0; s < KS; ++s)
+#pragma unroll
+      for (int i = 0; i < MT; ++i)
+#pragma unroll
+        for (int j = 0; j < NT; ++j)
+          acc[i][j] = Op16<TC>::mma16(__builtin_bit_cast(v8, af[s][i]), __builtin_bit_cast(v8, bfr[s][j]), acc[i][j]);
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  if (grp == 0) __builtin_amdgcn_s_barrier();  // matches group 1's extra barrier
+  __syncthreads();
+
+  // ---- epilogue: as gemm_kernel, per wave and 16-row strip through LDS
+  float* Cs = reinterpret_cast<float*>(lds) + wid * 16 * C::EPAD;
+  constexpr int CH = WN / 8;
+  const int rbase = m0 + grp * (BM / 2) + wm * WM, cbase = n0 + wn * WN;
+#pragma unroll
+  for (int i = 0; i < MT; ++i) {
+#pragma unroll
+    for (int j = 0; j < NT; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) Cs[(q * 4 + r) * C::EPAD + j * 16 + fr] = acc[i][j][r];
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    for (int idx = lane; idx < 16 * CH; idx += 64) {
+      const int rr = idx / CH, cc = idx % CH;
+      const int row = rbase + i * 16 + rr, col = cbase + cc * 8;
+      const float* sp = Cs + rr * C::EPAD + cc * 8;
+      float4 x0 = *reinterpret_cast<const float4*>(sp), x1 = *reinterpret_cast<const float4*>(sp + 4);
+      if (row < g.M && col < g.N) epi8<TC, EPI>(g, row, col, V8{{x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w}});
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  }
+  probe_exit(g.probe, probe_t);
+}
+
+template <typename TC, int EPI, int BM, int BN, int WGM2, int WGN2, int KS, int D>
+static void launch_pp(const GemmArgs& a, hipStream_t st) {
+  const int tiles = ((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN);
+  hipLaunchKernelGGL((gemm_pp_kernel<TC, EPI, BM, BN, WGM2, WGN2, KS, D>), dim3(tiles), dim3(512), 0, st, a);
+}
+
+// Tile configurations (16-bit operands; the fp32 parity mode always uses cfg 0):
+//   0: 64x128,  4 waves (2x2, 32x64 each),  3 stages, 2 blocks/CU
+//   1: 128x128, 4 waves (2x2, 64x64 each),  2 stages, 2 blocks/CU
+//   5: 192x128, 4 waves (2x2, 96x64 each),  2 stages, 2 blocks/CU
+//  11: 256x256 ping-pong, 8 waves as two groups of 4, 3-phase ring, 1 block/CU
+// (round 1 also measured 128x256, 192x256, 256x128, 256x256 4-wave forms and seven other
+// ping-pong geometries; none won a shape, so they are no longer built — DESIGN.md §3.)
+// Per-CU LDS-DMA intake (~37 B/clk) bounds the small tiles: bytes per MFLOP staged =
+// 64*(BM+BN)/(BM*BN) KB, so 64x128 -> 24, 128x128 -> 16, 256x256 -> 8.
+template <typename TC, int EPI, int BM, int BN, int WGM, int WGN, int NS, int KB = 128>
+static void launch_cfg(const GemmArgs& a, hipStream_t st) {
+  const int tiles = ((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN);
+  constexpr bool HOT = EPI == EPI_QKV || EPI == EPI_RESID || EPI == EPI_GELU_TANH || EPI == EPI_GELU_ERF_OP ||
+                       EPI == EPI_STORE;
+  if constexpr (HOT) {
+    if (a.N % BN == 0 && (EPI == EPI_QKV || a.ldc % 8 == 0)) {
+      hipLaunchKernelGGL((gemm_kernel<TC, EPI, BM, BN, WGM, WGN, NS, true, KB>), dim3(tiles), dim3(64 * WGM * WGN), 0,
+                         st, a);
+      return;
+    }
+  }
+  hipLaunchKernelGGL((gemm_kernel<TC, EPI, BM, BN, WGM, WGN, NS, false, KB>), dim3(tiles), dim3(64 * WGM * WGN), 0, st,
+                     a);
+}
+
+template <typename TC, int EPI>
+static hipError_t launch_t(const GemmArgs& a, hipStream_t st) {
+  if (a.M == 0) return hipSuccess;
+  int cfg = 0;
+  if constexpr (is16<TC>()) cfg = gemm_select_cfg(a);
+  switch (cfg) {
+    case 0: launch_cfg<TC, EPI, 64, 128, 2, 2, 3>(a, st); break;
+    case 1: launch_cfg<TC, EPI, 128, 128, 2, 2, 2>(a, st); break;
+    case 5: launch_cfg<TC, EPI, 192, 128, 2, 2, 2>(a, st); break;
+    default:
+      if constexpr (is16<TC>()) {
+        switch (cfg) {  // one 8-wave block per CU
+          case 2: launch_cfg<TC, EPI, 128, 256, 2, 4, 3>(a, st); return hipGetLastError();
+          case 3: launch_cfg<TC, EPI, 192, 256, 2, 4, 2>(a, st); return hipGetLastError();
+          case 4: launch_cfg<TC, EPI, 256, 128, 4, 2, 3>(a, st); return hipGetLastError();
+          case 6: launch_cfg<TC, EPI, 128, 128, 4, 2, 3>(a, st); return hipGetLastError();
+          case 7: launch_cfg<TC, EPI, 256, 256, 2, 4, 2>(a, st); return hipGetLastError();
+          case 8: launch_cfg<TC, EPI, 256, 192, 4, 2, 2>(a, st); return hipGetLastError();
+          case 9: launch_cfg<TC, EPI, 128, 128, 4, 2, 4>(a, st); return hipGetLastError();
+          // K32 stages (64-B rows), deep rings, two 4-wave blocks per CU (80 KB LDS each at most)
+          case 20: launch_cfg<TC, EPI, 64, 128, 2, 2, 6, 64>(a, st); return hipGetLastError();
+          case 21: launch_cfg<TC, EPI, 128, 128, 2, 2, 5, 64>(a, st); return hipGetLastError();
+          case 22: launch_cfg<TC, EPI, 192, 128, 2, 2, 4, 64>(a, st); return hipGetLastError();
+          case 23: launch_cfg<TC, EPI, 128, 192, 2, 2, 4, 64>(a, st); return hipGetLastError();
+          case 24: launch_cfg<TC, EPI, 128, 256, 2, 2, 3, 64>(a, st); return hipGetLastError();
+          default: break;
+        }
+        if (a.K % 64) return hipErrorInvalidValue;  // ping-pong: whole K64 phases
+        switch (cfg) {
+          case 11: launch_pp<TC, EPI, 256, 256, 1, 4, 1, 3>(a, st); break;
+          case 12: launch_pp<TC, EPI, 256, 192, 1, 4, 1, 3>(a, st); break;
+          case 14: launch_pp<TC, EPI, 256, 128, 2, 2, 1, 4>(a, st); break;
+          case 16: launch_pp<TC, EPI, 128, 128, 2, 2, 2, 3>(a, st); break;
+          default: return hipErrorInvalidValue;
+        }
+        break;
+      }
+      return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
+template <typename TC>
+static hipError_t launch_epi(int epi, const GemmArgs& a, hipStream_t st) {
+  switch (epi) {
+    case EPI_STORE: return launch_t<TC, EPI_STORE>(a, st);
+    case EPI_SILU: return launch_t<TC, EPI_SILU>(a, st);
+    case EPI_GELU_TANH: return launch_t<TC, EPI_GELU_TANH>(a, st);
+    case EPI_GELU_ERF: return launch_t<TC, EPI_GELU_ERF>(a, st);
+    case EPI_RESID: return launch_t<TC, EPI_RESID>(a, st);
+    case EPI_RESID_FILL: return launch_t<TC, EPI_RESID_FILL>(a, st);
+    case EPI_INPROJ: return launch_t<TC, EPI_INPROJ>(a, st);
+    case EPI_QKV: return launch_t<TC, EPI_QKV>(a, st);
+    case EPI_GELU_ERF_OP: return launch_t<TC, EPI_GELU_ERF_OP>(a, st);
+  }
+  return hipErrorInvalidValue;
+}
+
+
+}  // namespace f5h

@@ -32,6 +32,7 @@ EXPORTS = (
     "f5h_probe_enable",
     "f5h_probe_read",
     "f5h_set_graph_mode",
+    "f5h_set_cfg_streams",
     "f5h_graph_stats",
     "f5h_op_linear",
     "f5h_op_attention",
@@ -123,6 +124,8 @@ def lib():
     L.f5h_probe_read.restype = ctypes.c_int
     L.f5h_set_graph_mode.argtypes = [vp, i32]
     L.f5h_set_graph_mode.restype = ctypes.c_int
+    L.f5h_set_cfg_streams.argtypes = [vp, i32]
+    L.f5h_set_cfg_streams.restype = ctypes.c_int
     L.f5h_graph_stats.argtypes = [vp, ctypes.POINTER(i64), ctypes.POINTER(i64), ctypes.POINTER(i32)]
     L.f5h_graph_stats.restype = ctypes.c_int
     L.f5h_op_linear.argtypes = [vp, i32, i32, i32, i32, vp, vp, vp, vp, vp, sz]

@@ -101,6 +101,11 @@ class Engine:
         """True: the NFE loop replays one captured hipGraph step (default); False: eager launches."""
         _lib.check(_lib.lib().f5h_set_graph_mode(self._h, int(bool(on))), "set_graph_mode")
 
+    def set_cfg_streams(self, n: int):
+        """2: the captured step runs the two CFG branches as parallel launch chains; 1: one chain;
+        0: automatic (two chains for batches of >= 4 utterances, the default)."""
+        _lib.check(_lib.lib().f5h_set_cfg_streams(self._h, int(n)), "set_cfg_streams")
+
     def graph_stats(self):
         cap, rep, n = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int32()
         _lib.check(_lib.lib().f5h_graph_stats(self._h, ctypes.byref(cap), ctypes.byref(rep), ctypes.byref(n)),

@@ -20,6 +20,43 @@ from torch.nn.utils.rnn import pad_sequence
 from .utils import default, exists, lens_to_mask, list_str_to_idx, list_str_to_tensor, time_grid
 
 
+def _host_ints(x, batch):
+    """Python ints of a host-side length argument (int, list/tuple, CPU tensor), or None if on a device."""
+    if isinstance(x, int):
+        return [x] * batch
+    if isinstance(x, (list, tuple)):
+        return [int(v) for v in x]
+    if torch.is_tensor(x) and x.device.type == "cpu":
+        v = [int(a) for a in x.reshape(-1).tolist()]
+        return v * batch if len(v) == 1 else v
+    return None
+
+
+def _duration_rule_on_host(text, duration, lens, batch, cond_seq_len, max_duration):
+    """duration = clamp(max(max(#tokens, lens) + 1, duration), max_duration) (cfm.py:135-139) from host
+    values: exact whenever the token counts are on the host, and also for device-resident text when every
+    requested duration already exceeds the padded text width (#tokens <= text.shape[1]) and the prompt."""
+    dur = _host_ints(duration, batch)
+    ln = [cond_seq_len] * batch if lens is None else _host_ints(lens, batch)
+    if dur is None or ln is None or len(dur) != batch or len(ln) != batch:
+        return None
+    if text.device.type == "cpu":
+        ntok = (text != -1).sum(dim=-1).tolist()
+    elif all(d >= max(text.shape[1], lv) + 1 for d, lv in zip(dur, ln)):
+        ntok = [0] * batch  # the requested durations dominate whatever the counts are
+    else:
+        return None
+    return [min(max(max(int(t), lv) + 1, d), int(max_duration)) for t, lv, d in zip(ntok, ln, dur)]
+
+
+def _to_device(vals, device):
+    """Small host int list -> device LongTensor without a stream sync (pinned, non-blocking copy)."""
+    t = torch.tensor(vals, dtype=torch.long)
+    if torch.device(device).type == "cuda":
+        return t.pin_memory().to(device, non_blocking=True)
+    return t.to(device)
+
+
 class CFM(nn.Module):
     def __init__(self, transformer: nn.Module, sigma=0.0, odeint_kwargs: dict = dict(method="euler"),
                  audio_drop_prob=0.3, cond_drop_prob=0.2, num_channels=None, mel_spec_module: nn.Module | None = None,
@@ -76,23 +113,37 @@ class CFM(nn.Module):
             assert cond.shape[-1] == self.num_channels
         cond = cond.to(pdtype)
         batch, cond_seq_len, device = *cond.shape[:2], cond.device
-        if not exists(lens):
-            lens = torch.full((batch,), cond_seq_len, device=device, dtype=torch.long)
 
         if isinstance(text, list):
             if exists(self.vocab_char_map):
-                text = list_str_to_idx(text, self.vocab_char_map).to(device)
+                text = list_str_to_idx(text, self.vocab_char_map)
             else:
-                text = list_str_to_tensor(text).to(device)
+                text = list_str_to_tensor(text)
             assert text.shape[0] == batch
 
-        if isinstance(duration, int):
-            duration = torch.full((batch,), duration, device=device, dtype=torch.long)
-        duration = torch.maximum(torch.maximum((text != -1).sum(dim=-1), lens) + 1, duration)
-        duration = duration.clamp(max=max_duration)
-        # the one host sync of the preamble: every per-utterance length at once (the shapes below and
-        # the noise recipe need them on the host)
-        dur_host = [int(d) for d in duration.tolist()]
+        # The duration rule (cfm.py:132-139) decides the padded length, which the host needs. When the
+        # lengths are host values (ints, lists, CPU tensors) it is evaluated on the host and nothing waits
+        # for the device, so back-to-back calls keep the GPU busy; device-resident lengths take one sync.
+        dur_host = _duration_rule_on_host(text, duration, lens, batch, cond_seq_len, max_duration)
+        if dur_host is not None:
+            lens_host = [cond_seq_len] * batch if lens is None else _host_ints(lens, batch)
+            lens = _to_device(lens_host, device)
+            duration = _to_device(dur_host, device)
+            if text.device.type == "cpu" and torch.device(device).type == "cuda":
+                text = text.pin_memory().to(device, non_blocking=True)
+            else:
+                text = text.to(device)
+        else:
+            text = text.to(device)
+            if not exists(lens):
+                lens = torch.full((batch,), cond_seq_len, device=device, dtype=torch.long)
+            lens = lens.to(device)
+            if isinstance(duration, int):
+                duration = torch.full((batch,), duration, device=device, dtype=torch.long)
+            duration = torch.as_tensor(duration).to(device)
+            duration = torch.maximum(torch.maximum((text != -1).sum(dim=-1), lens) + 1, duration)
+            duration = duration.clamp(max=max_duration)
+            dur_host = [int(d) for d in duration.tolist()]  # the one host sync of this path
         max_duration = max(dur_host)
         if edit_mask is not None:
             cond_mask = lens_to_mask(lens) & edit_mask

@@ -115,9 +115,10 @@ def run_sharded(utts, sample_fn, *, rank: int, world: int, max_batch: int = 32, 
             cond = cond.to(device)
         text = [utts[i]["text"] for i in b]
         if torch.is_tensor(text[0]):  # token ids: one [B, nt] LongTensor, -1 padded (list_str_to_idx layout)
-            text = torch.nn.utils.rnn.pad_sequence(text, batch_first=True, padding_value=-1).to(cond.device)
-        dur = torch.tensor([utts[i]["total"] for i in b], dtype=torch.long, device=cond.device)
-        lens = torch.tensor([utts[i]["ref"] for i in b], dtype=torch.long, device=cond.device)
+            text = torch.nn.utils.rnn.pad_sequence(text, batch_first=True, padding_value=-1)
+        # lengths stay host tensors: CFM.sample evaluates its duration rule on the host without a sync
+        dur = torch.tensor([utts[i]["total"] for i in b], dtype=torch.long)
+        lens = torch.tensor([utts[i]["ref"] for i in b], dtype=torch.long)
         out = sample_fn(cond, text, dur, lens)
         for j, i in enumerate(b):
             local[i] = out[j, utts[i]["ref"]: utts[i]["total"]]

@@ -152,6 +152,12 @@ int f5h_probe_read(f5h_engine* eng, int64_t* launches, double* total_ms);
  * Results are bitwise identical in both modes. f5h_graph_stats: captures so far, step replays so
  * far, graphs cached (LRU, at most 8; an evicted graph is destroyed only after its last user). */
 int f5h_set_graph_mode(f5h_engine* eng, int32_t mode);
+/* Launch chains of the captured step: 2 captures the conditional and the unconditional CFG branch as
+ * two parallel chains (fork/join by events), so kernel boundaries of one branch overlap work of the
+ * other; 1 = one chain over the packed batch; 0 = automatic (default: two chains for batches of 4 or
+ * more utterances; env F5H_SPLIT_CFG=0/1/2 = never/always/auto at engine creation). Results are
+ * bitwise identical. */
+int f5h_set_cfg_streams(f5h_engine* eng, int32_t n);
 int f5h_graph_stats(f5h_engine* eng, int64_t* captures, int64_t* replays, int32_t* cached);
 
 /* Op-level entry points (parity tests / microbenchmarks). Device pointers, row-major. */

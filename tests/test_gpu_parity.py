@@ -7,6 +7,8 @@ Tolerances (written here, BASELINE north star: "within 1e-3 rel fp32"):
     <= 1.5 x the reference's OWN bf16 / fp16 error vs its fp32 output.
 """
 
+import os
+
 import numpy as np
 import pytest
 import torch
@@ -66,6 +68,8 @@ def test_op_linear(compute, tol, M, N, K):
 
 
 GEMM_CONFIGS = [0, 1, 5, 11]  # 11: ping-pong 8-wave 256x256 kernel
+if os.environ.get("F5H_TEST_GEMM_CFGS"):  # tuning runs: check extra configurations too
+    GEMM_CONFIGS = [int(c) for c in os.environ["F5H_TEST_GEMM_CFGS"].split(",")]
 
 
 @pytest.mark.parametrize("compute", ["bf16", "fp16"])

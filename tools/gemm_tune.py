@@ -16,10 +16,11 @@ SHAPES = {  # name: (M, N, K); C2 = 2 x 1876 rows, C3 = 64 x 1876 rows
     "c2_qkv": (3752, 3072, 1024), "c2_ffn1": (3752, 2048, 1024), "c2_out": (3752, 1024, 1024),
     "c2_ffn2": (3752, 1024, 2048), "c3_qkv": (120064, 3072, 1024), "c3_ffn2": (120064, 1024, 2048),
 }
-CFGS = {0: (64, 128, 256), 1: (128, 128, 256), 2: (128, 256, 512), 3: (192, 256, 512), 4: (256, 128, 512),
-        5: (192, 128, 256), 6: (128, 128, 512), 7: (256, 256, 512),
-        10: (256, 256, 512), 11: (256, 192, 512), 12: (256, 128, 512), 13: (128, 128, 512), 14: (128, 128, 512),
-        15: (256, 64, 512), 16: (128, 256, 512), 17: (256, 256, 512)}
+CFGS = {0: (64, 128, 256), 1: (128, 128, 256), 5: (192, 128, 256),
+        2: (128, 256, 512), 3: (192, 256, 512), 4: (256, 128, 512), 6: (128, 128, 512), 7: (256, 256, 512),
+        8: (256, 192, 512), 9: (128, 128, 512),
+        11: (256, 256, 512), 12: (256, 192, 512), 14: (256, 128, 512), 16: (128, 128, 512),
+        20: (64, 128, 256), 21: (128, 128, 256), 22: (192, 128, 256), 23: (128, 192, 256), 24: (128, 256, 256)}
 REPS = 20
 if os.environ.get("GT_CFGS"):  # e.g. GT_CFGS=5,11 GT_SHAPES=c3_qkv,c3_ffn2
     CFGS = {int(c): CFGS[int(c)] for c in os.environ["GT_CFGS"].split(",")}

@@ -1,0 +1,90 @@
+"""HBM traffic per launch of each kernel class of the C2 step, from rocprofv3 PMC passes.
+
+Per pass one counter (MI355X_MICROARCH.md §rocprofv3 PMC slots: FETCH_SIZE uses 3 TCC slots,
+WRITE_SIZE 2, so they cannot share a pass):
+    rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmc_f -o run -- python tools/trace_c2.py run
+    rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmc_w -o run -- python tools/trace_c2.py run
+    python tools/pmc_classes.py gpurun_out/pmc_f/run_counter_collection.csv \
+        gpurun_out/pmc_w/run_counter_collection.csv profiles/r02_pmc_classes.json
+
+Dispatches are classified by their position around each attention dispatch (one DiT block issues
+norm1, qkv, attention, out, norm, ffn1, ffn2 in that order). hbm_bytes = 2 x FETCH_SIZE (gfx950
+counts half of wide streaming reads) + WRITE_SIZE, in bytes (the counters report KB), median over
+the dispatches of the class. algorithmic_bytes: operands + results at their widths (C2 shapes).
+"""
+import csv
+import json
+import statistics
+import sys
+from collections import defaultdict
+
+ORDER = {-2: "norm1", -1: "qkv", 1: "out", 2: "norm", 3: "ffn1", 4: "ffn2"}
+
+
+def load(path, counter):
+    rows = {}
+    for r in csv.DictReader(open(path)):
+        if r.get("Counter_Name") != counter:
+            continue
+        did = int(r["Dispatch_Id"])
+        rows[did] = (r["Kernel_Name"], rows.get(did, (None, 0.0))[1] + float(r["Counter_Value"]))
+    return [(d, n, v) for d, (n, v) in sorted(rows.items())]
+
+
+def classify(disp):
+    cls = {}
+    for i, (_, name, _) in enumerate(disp):
+        if "attn16" in name or "attn_f32" in name:
+            cls[i] = "attention"
+            for off, c in ORDER.items():
+                if 0 <= i + off < len(disp):
+                    cls.setdefault(i + off, c)
+        elif "conv_kernel" in name:
+            cls[i] = "conv"
+    return cls
+
+
+def algorithmic(c, S=2, L=1876, d=1024, ff=2048, H=16, es=2):
+    rows = S * L
+    gemm = {"qkv": (d, 3 * d, es), "out": (d, d, 8), "ffn1": (d, ff, es), "ffn2": (ff, d, 8)}
+    if c in gemm:
+        K, N, out_b = gemm[c]
+        return es * (rows * K + N * K) + out_b * rows * N
+    if c == "attention":
+        return 4 * es * S * H * L * 64  # q, k, v read + o written
+    if c in ("norm", "norm1"):
+        return rows * d * (4 + es)
+    return None
+
+
+def main(fpath, wpath, out):
+    f = load(fpath, "FETCH_SIZE")
+    w = load(wpath, "WRITE_SIZE")
+    cf, cw = classify(f), classify(w)
+    acc = defaultdict(lambda: {"f": [], "w": []})
+    for i, (_, _, v) in enumerate(f):
+        if i in cf:
+            acc[cf[i]]["f"].append(v)
+    for i, (_, _, v) in enumerate(w):
+        if i in cw:
+            acc[cw[i]]["w"].append(v)
+    res = {}
+    for c, a in acc.items():
+        if not a["f"] or not a["w"]:
+            continue
+        fk, wk = statistics.median(a["f"]), statistics.median(a["w"])
+        hbm = (2.0 * fk + wk) * 1024.0
+        alg = algorithmic(c)
+        res[c] = {"fetch_size_kb": fk, "write_size_kb": wk, "dispatches": len(a["f"]), "hbm_bytes": hbm,
+                  "algorithmic_bytes": alg, "hbm_over_algorithmic": round(hbm / alg, 3) if alg else None}
+    j = {"note": "C2 step (F5TTS_v1_Base, S=2, N=1876, bf16), rocprofv3 --pmc one counter per pass over 3 "
+                 "CFM.sample calls (tools/trace_c2.py run); median per dispatch; hbm_bytes = "
+                 "(2*FETCH_SIZE + WRITE_SIZE) * 1024 (gfx950 FETCH_SIZE reads half of wide streaming reads, "
+                 "MI355X_MICROARCH.md HBM section); FETCH counts Infinity-Cache hits too",
+         "classes": res}
+    json.dump(j, open(out, "w"), indent=1)
+    print(json.dumps(j, indent=1))
+
+
+if __name__ == "__main__":
+    main(*sys.argv[1:4])
