@@ -134,10 +134,15 @@ PROBE_CLASSES = ("qkv", "attention", "out", "norm", "ffn1", "ffn2", "conv")
 PEAK_HBM_GBPS = 8000.0
 
 
-def class_entry(kc, avg_ms, n, arch, S, L, launches_per_call, ms_call):
+def class_entry(kc, avg_ms, n, arch, S, L, launches_per_call, ms_call, chains=1):
+    """One kernel class: algorithmic work per launch slot / average launch span. With the two CFG
+    chains captured in parallel (chains = 2, batches of >= 4 utterances) each chain launches the class
+    on half the sequences and the two chains' launches of a class overlap in time, so a slot (the span
+    of one launch) covers both halves: flops are counted for all S sequences and the slot count is per
+    chain."""
     fl = class_flops(kc, arch, S, L)
     e = {"kernel": kc, "avg_launch_us": round(avg_ms * 1e3, 3), "sampled_launches": n,
-         "launches_per_call": launches_per_call,
+         "launches_per_call": launches_per_call, "cfg_chains": chains,
          "share_of_call": round(avg_ms * launches_per_call / ms_call, 4) if ms_call else None}
     if fl:
         ach = fl / (avg_ms * 1e-3) / 1e12
@@ -234,6 +239,7 @@ def main():
 
     eng = model.transformer.get_engine(model.engine_compute(), device)
     S = 2 * B if case["cfg"] >= 1e-5 else B
+    chains = 2 if (case["cfg"] >= 1e-5 and B >= 4) else 1  # the engine's automatic CFG-branch split
     L = Nmax if arch["backbone"] == "DiT" else Nmax + 1
     launches = {"norm": arch["depth"]}
     for kc in ("qkv", "attention", "out", "ffn1", "ffn2"):
@@ -258,7 +264,7 @@ def main():
         n, ms = eng.probe_read()
         eng.probe(None)
         if n:
-            classes[kc] = class_entry(kc, ms / n, n, arch, S, L, launches[kc] * case["nfe"], ms_pre)
+            classes[kc] = class_entry(kc, ms / n, n, arch, S, L, launches[kc] * case["nfe"], ms_pre, chains)
     probe = args.probe
     if probe == "auto":
         probe = max(classes, key=lambda k: classes[k]["share_of_call"] or 0.0) if classes else "none"
@@ -284,7 +290,7 @@ def main():
         eng.probe(None)
         if n_launch:
             roof = class_entry(probe, probe_ms / n_launch, n_launch, arch, S, L, launches[probe] * case["nfe"],
-                               elapsed / args.steps * 1e3)
+                               elapsed / args.steps * 1e3, chains)
             roof["timing"] = ("in-kernel s_memrealtime stamps: first workgroup start to last wave end of every "
                               "launch of the class in every 4th ODE step inside the timed region")
     if world > 1:

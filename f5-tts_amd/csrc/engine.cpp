@@ -1134,8 +1134,8 @@ int f5h_op_linear(void* stream, int32_t compute, int32_t M, int32_t N, int32_t K
 }
 
 int f5h_gemm_force_config(int32_t cfg) {
-  if (cfg < -1 || cfg > 24 || cfg == 10 || cfg == 13 || cfg == 15 || (cfg > 16 && cfg < 20))
-    return fail(F5H_EINVAL, "gemm config must be -1, 0..9, 11, 12, 14, 16 or 20..24");
+  if (cfg != -1 && cfg != 0 && cfg != 1 && cfg != 5 && cfg != 11)
+    return fail(F5H_EINVAL, "gemm config must be -1, 0, 1, 5 or 11");
   gemm_force_config(cfg);
   g_kernel_epoch.fetch_add(1);
   return 0;

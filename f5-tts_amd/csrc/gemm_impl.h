@@ -793,30 +793,8 @@ static hipError_t launch_t(const GemmArgs& a, hipStream_t st) {
     case 5: launch_cfg<TC, EPI, 192, 128, 2, 2, 2>(a, st); break;
     default:
       if constexpr (is16<TC>()) {
-        switch (cfg) {  // one 8-wave block per CU
-          case 2: launch_cfg<TC, EPI, 128, 256, 2, 4, 3>(a, st); return hipGetLastError();
-          case 3: launch_cfg<TC, EPI, 192, 256, 2, 4, 2>(a, st); return hipGetLastError();
-          case 4: launch_cfg<TC, EPI, 256, 128, 4, 2, 3>(a, st); return hipGetLastError();
-          case 6: launch_cfg<TC, EPI, 128, 128, 4, 2, 3>(a, st); return hipGetLastError();
-          case 7: launch_cfg<TC, EPI, 256, 256, 2, 4, 2>(a, st); return hipGetLastError();
-          case 8: launch_cfg<TC, EPI, 256, 192, 4, 2, 2>(a, st); return hipGetLastError();
-          case 9: launch_cfg<TC, EPI, 128, 128, 4, 2, 4>(a, st); return hipGetLastError();
-          // K32 stages (64-B rows), deep rings, two 4-wave blocks per CU (80 KB LDS each at most)
-          case 20: launch_cfg<TC, EPI, 64, 128, 2, 2, 6, 64>(a, st); return hipGetLastError();
-          case 21: launch_cfg<TC, EPI, 128, 128, 2, 2, 5, 64>(a, st); return hipGetLastError();
-          case 22: launch_cfg<TC, EPI, 192, 128, 2, 2, 4, 64>(a, st); return hipGetLastError();
-          case 23: launch_cfg<TC, EPI, 128, 192, 2, 2, 4, 64>(a, st); return hipGetLastError();
-          case 24: launch_cfg<TC, EPI, 128, 256, 2, 2, 3, 64>(a, st); return hipGetLastError();
-          default: break;
-        }
-        if (a.K % 64) return hipErrorInvalidValue;  // ping-pong: whole K64 phases
-        switch (cfg) {
-          case 11: launch_pp<TC, EPI, 256, 256, 1, 4, 1, 3>(a, st); break;
-          case 12: launch_pp<TC, EPI, 256, 192, 1, 4, 1, 3>(a, st); break;
-          case 14: launch_pp<TC, EPI, 256, 128, 2, 2, 1, 4>(a, st); break;
-          case 16: launch_pp<TC, EPI, 128, 128, 2, 2, 2, 3>(a, st); break;
-          default: return hipErrorInvalidValue;
-        }
+        if (cfg != 11 || a.K % 64) return hipErrorInvalidValue;  // ping-pong: whole K64 phases
+        launch_pp<TC, EPI, 256, 256, 1, 4, 1, 3>(a, st);
         break;
       }
       return hipErrorInvalidValue;

@@ -35,6 +35,7 @@ class Vocos:
         self._state = None
         self._h = None
         self._lock = threading.Lock()
+        self._create_lock = threading.Lock()
         self._ws = {}
 
     # ------------------------------------------------------------------ nn.Module-like surface
@@ -59,6 +60,12 @@ class Vocos:
         return self
 
     def _engine(self):
+        # decode() is called from the reference's thread pool (utils_infer.py:540-547): create the engine
+        # under a lock so concurrent first calls build (and upload weights for) exactly one
+        with self._create_lock:
+            return self._engine_locked()
+
+    def _engine_locked(self):
         if self._h is not None:
             return self._h
         if self._state is None:

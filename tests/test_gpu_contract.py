@@ -298,3 +298,34 @@ def test_edge_sample_fp16(name):
     torch.cuda.synchronize()
     assert np.asarray(out.shape).tolist() == list(g["out"].shape)
     assert gc.rel_err(out.float().cpu().numpy(), g["out"]) < 2e-2
+
+
+@pytest.mark.parametrize("compute", ["bf16", "fp32"])
+def test_cfg_branch_chains_bitwise_equal(compute):
+    """The step graph with the conditional and unconditional CFG branches captured as two parallel
+    launch chains (the default for batches of >= 4 utterances) gives bitwise the result of one chain
+    over the packed batch, and of the eager launch sequence."""
+    _need_gpu()
+    m = _model(gc.arch_of("tiny"), compute)
+    spec = dict(B=5, ref_frames=[40, 60, 25, 33, 51], total_frames=[90, 150, 70, 120, 101], n_text=[20, 30, 12, 9, 25],
+                vocab=64)
+    inp = synthetic.make_case(**spec)
+    dur = torch.maximum(torch.maximum((inp["text"] != -1).sum(-1), inp["lens"]) + 1, inp["duration"])
+    y0 = synthetic.reference_noise(dur, 2).to(DEV)
+    eng = m.transformer.get_engine(compute, m.device)
+    kw = dict(cond=inp["cond"].to(DEV), text=inp["text"].to(DEV), duration=inp["duration"], lens=inp["lens"],
+              steps=5, cfg_strength=2.0, sway_sampling_coef=-1.0, y0=y0)
+    outs = {}
+    try:
+        for mode in ("one", "two", "eager"):
+            eng.set_graph_mode(mode != "eager")
+            eng.set_cfg_streams(2 if mode == "two" else 1)
+            out, traj = m.sample(**kw)
+            torch.cuda.synchronize()
+            outs[mode] = (out.clone(), traj.clone())
+    finally:
+        eng.set_graph_mode(True)
+        eng.set_cfg_streams(0)
+    for mode in ("two", "eager"):
+        assert torch.equal(outs[mode][0], outs["one"][0]), mode
+        assert torch.equal(outs[mode][1], outs["one"][1]), mode

@@ -16,11 +16,10 @@ SHAPES = {  # name: (M, N, K); C2 = 2 x 1876 rows, C3 = 64 x 1876 rows
     "c2_qkv": (3752, 3072, 1024), "c2_ffn1": (3752, 2048, 1024), "c2_out": (3752, 1024, 1024),
     "c2_ffn2": (3752, 1024, 2048), "c3_qkv": (120064, 3072, 1024), "c3_ffn2": (120064, 1024, 2048),
 }
-CFGS = {0: (64, 128, 256), 1: (128, 128, 256), 5: (192, 128, 256),
-        2: (128, 256, 512), 3: (192, 256, 512), 4: (256, 128, 512), 6: (128, 128, 512), 7: (256, 256, 512),
-        8: (256, 192, 512), 9: (128, 128, 512),
-        11: (256, 256, 512), 12: (256, 192, 512), 14: (256, 128, 512), 16: (128, 128, 512),
-        20: (64, 128, 256), 21: (128, 128, 256), 22: (192, 128, 256), 23: (128, 192, 256), 24: (128, 256, 256)}
+CFGS = {0: (64, 128, 256), 1: (128, 128, 256), 5: (192, 128, 256), 11: (256, 256, 512)}
+# round 2 also timed 8-wave one-block-per-CU tiles (128x256, 192x256, 256x128, 128x128, 256x256, 256x192),
+# K32-stage deep rings (64x128..128x256) and DMA issue interleaved with the MFMAs; all slower at C2
+# (profiles/r02_gemm_tune_c2*.txt), so they are no longer built.
 REPS = 20
 if os.environ.get("GT_CFGS"):  # e.g. GT_CFGS=5,11 GT_SHAPES=c3_qkv,c3_ffn2
     CFGS = {int(c): CFGS[int(c)] for c in os.environ["GT_CFGS"].split(",")}

@@ -29,8 +29,9 @@ def run(config="c2", calls=3):
     refs = case["ref"] if isinstance(case["ref"], list) else [case["ref"]] * B
     tots = case["total"] if isinstance(case["total"], list) else [case["total"]] * B
     inp = synthetic.make_case(B=B, ref_frames=refs, total_frames=tots, n_text=case["nt"])
-    kw = dict(cond=inp["cond"].to(dev), text=inp["text"].to(dev), duration=inp["duration"].to(dev),
-              lens=inp["lens"].to(dev), steps=case["nfe"], cfg_strength=case["cfg"],
+    # lengths as host tensors (as the DP driver passes them): no device sync inside the calls
+    kw = dict(cond=inp["cond"].to(dev), text=inp["text"].to(dev), duration=inp["duration"],
+              lens=inp["lens"], steps=case["nfe"], cfg_strength=case["cfg"],
               sway_sampling_coef=case["sway"], seed=0, keep_trajectory=False)
     for _ in range(3):
         model.sample(**kw)
