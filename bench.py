@@ -222,7 +222,8 @@ def main():
     utts = build_job(case, world)
     for u in utts:  # inputs resident in HBM before anything is timed
         u["cond"], u["text"] = u["cond"].to(device), u["text"].to(device)
-    batches = parallel.plan([u["total"] for u in utts], world, max_batch=B)[rank]
+    plan_all = parallel.plan([u["total"] for u in utts], world, max_batch=B)
+    batches = plan_all[rank]
     my = [i for b in batches for i in b]
     gen_frames = sum(utts[i]["total"] - utts[i]["ref"] for i in my)
     job_frames = sum(u["total"] - u["ref"] for u in utts)
@@ -235,7 +236,7 @@ def main():
         return out
 
     def step():
-        return parallel.run_sharded(utts, sample, rank=rank, world=world, device=device, batches=batches)
+        return parallel.run_sharded(utts, sample, rank=rank, world=world, device=device, plan_all=plan_all)
 
     eng = model.transformer.get_engine(model.engine_compute(), device)
     S = 2 * B if case["cfg"] >= 1e-5 else B
@@ -313,7 +314,7 @@ def main():
         voc = Vocos(compute="bf16")
         voc.load_state_dict(vocos_weights())
         voc.to(device)
-        mels = parallel.run_sharded(utts, sample, rank=rank, world=1, device=device, batches=batches)
+        mels = parallel.run_sharded(utts, sample, rank=0, world=1, device=device, plan_all=[batches])
         gens = [mels[i].t().unsqueeze(0).float().contiguous() for i in my]
         for g in gens:
             voc.decode(g)

@@ -52,10 +52,25 @@ def bucket(indices, frames, max_batch: int):
     return [idx[k:k + max_batch] for k in range(0, len(idx), max_batch)]
 
 
-def gather_mels(local: "dict[int, torch.Tensor]", device=None, group=None):
+def gather_mels(local: "dict[int, torch.Tensor]", device=None, group=None, layout=None):
     """All-gather finished mels {utt_index: [n_i, C]} from every rank.
-    Returns {utt_index: tensor} with every utterance of the job (on every rank)."""
+    Returns {utt_index: tensor} with every utterance of the job (on every rank).
+
+    layout: per rank, the [(utt_index, n_frames), ...] it holds, when every rank knows the plan
+    (run_sharded does): then only the padded mel buffers travel and no count or index is read back
+    to the host, so the gather never waits for the device."""
     world = dist.get_world_size(group)
+    if layout is not None:
+        dev = device if device is not None else next(iter(local.values())).device
+        C = next(iter(local.values())).shape[-1] if local else 100
+        maxn = max(len(x) for x in layout)
+        maxl = max((n for x in layout for _, n in x), default=0)
+        buf = torch.zeros(maxn, maxl, C, dtype=torch.float32, device=dev)
+        for j, (k, n) in enumerate(layout[dist.get_rank(group)]):
+            buf[j, :n] = local[k].float()
+        bufs = [torch.empty_like(buf) for _ in range(world)]
+        dist.all_gather(bufs, buf, group=group)
+        return {k: bufs[r][j, :n] for r in range(world) for j, (k, n) in enumerate(layout[r])}
     dev = device if device is not None else (next(iter(local.values())).device if local else torch.device("cpu"))
     C = next(iter(local.values())).shape[-1] if local else 100
     keys = sorted(local)
@@ -97,17 +112,18 @@ def plan(totals, world: int, max_batch: int):
 
 
 def run_sharded(utts, sample_fn, *, rank: int, world: int, max_batch: int = 32, device=None, group=None,
-                batches=None):
+                plan_all=None):
     """Run a whole utterance job data-parallel and return {index: generated mel [total-ref, C]} on
     every rank.
 
     utts: list of dicts with `cond` [ref_i(, padded), C] mel, `text` (str list or id list), `ref` (prompt
     frames) and `total` (total frames), the fields of one prompt in eval_infer_batch.py:182-185.
     sample_fn(cond [B,Nc,C], text list, duration LongTensor[B], lens LongTensor[B]) -> out [B,N,C]: the
-    engine's `CFM.sample` (or a stand-in in tests). `batches` (from `plan`) may be passed to reuse a
-    plan across calls. World 1 runs without any collective."""
-    if batches is None:
-        batches = plan([u["total"] for u in utts], world, max_batch)[rank]
+    engine's `CFM.sample` (or a stand-in in tests). `plan_all` (from `plan`, every rank's batches) may be
+    passed to reuse a plan across calls. World 1 runs without any collective."""
+    if plan_all is None:
+        plan_all = plan([u["total"] for u in utts], world, max_batch)
+    batches = plan_all[rank]
     local = {}
     for b in batches:
         cond = padded_mel_batch([utts[i]["cond"][: utts[i]["ref"]] for i in b])
@@ -124,5 +140,6 @@ def run_sharded(utts, sample_fn, *, rank: int, world: int, max_batch: int = 32, 
             local[i] = out[j, utts[i]["ref"]: utts[i]["total"]]
     if world == 1:
         return local
-    return gather_mels(local, device=device, group=group)
+    layout = [[(i, utts[i]["total"] - utts[i]["ref"]) for b in plan_all[r] for i in b] for r in range(world)]
+    return gather_mels(local, device=device, group=group, layout=layout)
 
