@@ -124,87 +124,129 @@ hipError_t silu_to_op(int compute, const float* x, void* y, int64_t n, hipStream
 }
 
 // ---------------------------------------------------------------- norms
-// One wave per row, row cached in registers (d <= 2048, d % 4 == 0).
+// One wave per row, row cached in registers. NV = float4 per lane: compile-time for the widths the
+// path uses (d = 256*NV), so every load is unconditional; d <= 2048, d % 4 == 0 otherwise.
 constexpr int MAXV = 8;  // float4 per lane
 
+// Row sum over the wave, the same value in every lane: DPP butterflies inside each 16-lane row
+// (xor 1, xor 2, half-mirror, mirror: VALU, no LDS round trip), then the four row sums by readlane.
+F5H_DEV float wave_sum_dpp(float v) {
+  auto dpp = [](float x, int ctrl) -> float {
+    switch (ctrl) {  // the control word must be an immediate
+      case 0xB1: return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0xB1, 0xF, 0xF, false));
+      case 0x4E: return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0x4E, 0xF, 0xF, false));
+      case 0x141: return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0x141, 0xF, 0xF, false));
+      default: return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0x140, 0xF, 0xF, false));
+    }
+  };
+  v += dpp(v, 0xB1);   // quad_perm [1,0,3,2]
+  v += dpp(v, 0x4E);   // quad_perm [2,3,0,1]
+  v += dpp(v, 0x141);  // row_half_mirror
+  v += dpp(v, 0x140);  // row_mirror: every lane of a row holds the row sum
+  const float r0 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 0));
+  const float r1 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 16));
+  const float r2 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 32));
+  const float r3 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 48));
+  return (r0 + r1) + (r2 + r3);
+}
+
 // LayerNorm(no affine, eps 1e-6) * (1 + scale) + shift (AdaLayerNorm modules.py:325, ff_norm :753,
-// AdaLayerNorm_Final :346)
-template <typename TO>
-__global__ void ln_mod_kernel(const float* h, int M, int d, const float* shift, const float* scale, TO* out) {
+// AdaLayerNorm_Final :346). The modulation rows are loaded with the row, before the reductions.
+template <typename TO, int NV>
+__global__ __launch_bounds__(256) void ln_mod_kernel(const float* h, int M, int d, const float* shift,
+                                                     const float* scale, TO* out) {
+  constexpr bool FIXED = NV > 0;
+  constexpr int V = FIXED ? NV : MAXV;
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
   if (row >= M) return;
   const float4* x = reinterpret_cast<const float4*>(h + (int64_t)row * d);
-  const int n4 = d >> 2;
-  float4 v[MAXV];
-  float s = 0.f;
-#pragma unroll
-  for (int k = 0; k < MAXV; ++k) {
-    int i = lane + 64 * k;
-    v[k] = i < n4 ? x[i] : make_float4(0, 0, 0, 0);
-    s += v[k].x + v[k].y + v[k].z + v[k].w;
-  }
-  const float mean = wave_sum(s) / d;
-  float q = 0.f;
-#pragma unroll
-  for (int k = 0; k < MAXV; ++k) {
-    int i = lane + 64 * k;
-    if (i < n4) {
-      float a = v[k].x - mean, b = v[k].y - mean, c = v[k].z - mean, e = v[k].w - mean;
-      q += a * a + b * b + c * c + e * e;
-    }
-  }
-  const float rstd = rsqrtf(wave_sum(q) / d + 1e-6f);
   const float4* sh = reinterpret_cast<const float4*>(shift);
   const float4* sc = reinterpret_cast<const float4*>(scale);
+  const int n4 = FIXED ? 64 * NV : d >> 2;
+  float4 v[V], a[V], b[V];
 #pragma unroll
-  for (int k = 0; k < MAXV; ++k) {
-    int i = lane + 64 * k;
-    if (i < n4) {
-      float4 a = sc[i], b = sh[i];
-      store4<TO>(out + (int64_t)row * d + 4 * i, (v[k].x - mean) * rstd * (1.f + a.x) + b.x,
-                 (v[k].y - mean) * rstd * (1.f + a.y) + b.y, (v[k].z - mean) * rstd * (1.f + a.z) + b.z,
-                 (v[k].w - mean) * rstd * (1.f + a.w) + b.w);
+  for (int k = 0; k < V; ++k) {
+    const int i = lane + 64 * k;
+    const bool ok = FIXED || i < n4;
+    v[k] = ok ? x[i] : make_float4(0, 0, 0, 0);
+    a[k] = ok ? sc[i] : make_float4(0, 0, 0, 0);
+    b[k] = ok ? sh[i] : make_float4(0, 0, 0, 0);
+  }
+  float s = 0.f;
+#pragma unroll
+  for (int k = 0; k < V; ++k) s += v[k].x + v[k].y + v[k].z + v[k].w;
+  const float mean = wave_sum_dpp(s) / d;
+  float q = 0.f;
+#pragma unroll
+  for (int k = 0; k < V; ++k) {
+    const int i = lane + 64 * k;
+    if (FIXED || i < n4) {
+      float p0 = v[k].x - mean, p1 = v[k].y - mean, p2 = v[k].z - mean, p3 = v[k].w - mean;
+      q += p0 * p0 + p1 * p1 + p2 * p2 + p3 * p3;
     }
+  }
+  const float rstd = rsqrtf(wave_sum_dpp(q) / d + 1e-6f);
+#pragma unroll
+  for (int k = 0; k < V; ++k) {
+    const int i = lane + 64 * k;
+    if (FIXED || i < n4)
+      store4<TO>(out + (int64_t)row * d + 4 * i, (v[k].x - mean) * rstd * (1.f + a[k].x) + b[k].x,
+                 (v[k].y - mean) * rstd * (1.f + a[k].y) + b[k].y, (v[k].z - mean) * rstd * (1.f + a[k].z) + b[k].z,
+                 (v[k].w - mean) * rstd * (1.f + a[k].w) + b[k].w);
   }
 }
 hipError_t ln_modulate(int compute, const float* h, int M, int d, const float* shift, const float* scale, void* out,
                        hipStream_t st) {
   if (d % 4 || d > 4 * 64 * MAXV) return hipErrorInvalidValue;
-  F5H_OP_DISPATCH(compute, T, hipLaunchKernelGGL(ln_mod_kernel<T>, dim3(nblk(M, 4)), dim3(256), 0, st, h, M, d, shift, scale, (T*)out););
+  const dim3 g(nblk(M, 4)), b(256);
+  switch (d) {
+    case 1024: F5H_OP_DISPATCH(compute, T, hipLaunchKernelGGL((ln_mod_kernel<T, 4>), g, b, 0, st, h, M, d, shift, scale, (T*)out);); break;
+    case 768: F5H_OP_DISPATCH(compute, T, hipLaunchKernelGGL((ln_mod_kernel<T, 3>), g, b, 0, st, h, M, d, shift, scale, (T*)out);); break;
+    case 512: F5H_OP_DISPATCH(compute, T, hipLaunchKernelGGL((ln_mod_kernel<T, 2>), g, b, 0, st, h, M, d, shift, scale, (T*)out);); break;
+    default: F5H_OP_DISPATCH(compute, T, hipLaunchKernelGGL((ln_mod_kernel<T, 0>), g, b, 0, st, h, M, d, shift, scale, (T*)out););
+  }
   return hipGetLastError();
 }
 
 // x_transformers RMSNorm: F.normalize(x, dim=-1) * sqrt(d) * g (unett.py:156,160,185)
-template <typename TO>
-__global__ void rms_kernel(const float* h, int M, int d, const float* g, TO* out) {
+template <typename TO, int NV>
+__global__ __launch_bounds__(256) void rms_kernel(const float* h, int M, int d, const float* g, TO* out) {
+  constexpr bool FIXED = NV > 0;
+  constexpr int V = FIXED ? NV : MAXV;
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
   if (row >= M) return;
   const float4* x = reinterpret_cast<const float4*>(h + (int64_t)row * d);
-  const int n4 = d >> 2;
-  float4 v[MAXV];
+  const float4* gg = reinterpret_cast<const float4*>(g);
+  const int n4 = FIXED ? 64 * NV : d >> 2;
+  float4 v[V], a[V];
   float q = 0.f;
 #pragma unroll
-  for (int k = 0; k < MAXV; ++k) {
-    int i = lane + 64 * k;
-    v[k] = i < n4 ? x[i] : make_float4(0, 0, 0, 0);
-    q += v[k].x * v[k].x + v[k].y * v[k].y + v[k].z * v[k].z + v[k].w * v[k].w;
+  for (int k = 0; k < V; ++k) {
+    const int i = lane + 64 * k;
+    const bool ok = FIXED || i < n4;
+    v[k] = ok ? x[i] : make_float4(0, 0, 0, 0);
+    a[k] = ok ? gg[i] : make_float4(0, 0, 0, 0);
   }
-  const float nrm = fmaxf(sqrtf(wave_sum(q)), 1e-12f);
-  const float f = sqrtf((float)d);
-  const float4* gg = reinterpret_cast<const float4*>(g);
 #pragma unroll
-  for (int k = 0; k < MAXV; ++k) {
-    int i = lane + 64 * k;
-    if (i < n4) {
-      float4 a = gg[i];
-      store4<TO>(out + (int64_t)row * d + 4 * i, v[k].x / nrm * f * a.x, v[k].y / nrm * f * a.y,
-                 v[k].z / nrm * f * a.z, v[k].w / nrm * f * a.w);
-    }
+  for (int k = 0; k < V; ++k) q += v[k].x * v[k].x + v[k].y * v[k].y + v[k].z * v[k].z + v[k].w * v[k].w;
+  const float nrm = fmaxf(sqrtf(wave_sum_dpp(q)), 1e-12f);
+  const float f = sqrtf((float)d);
+#pragma unroll
+  for (int k = 0; k < V; ++k) {
+    const int i = lane + 64 * k;
+    if (FIXED || i < n4)
+      store4<TO>(out + (int64_t)row * d + 4 * i, v[k].x / nrm * f * a[k].x, v[k].y / nrm * f * a[k].y,
+                 v[k].z / nrm * f * a[k].z, v[k].w / nrm * f * a[k].w);
   }
 }
 hipError_t rms_norm_g(int compute, const float* h, int M, int d, const float* g, void* out, hipStream_t st) {
   if (d % 4 || d > 4 * 64 * MAXV) return hipErrorInvalidValue;
-  F5H_OP_DISPATCH(compute, T, hipLaunchKernelGGL(rms_kernel<T>, dim3(nblk(M, 4)), dim3(256), 0, st, h, M, d, g, (T*)out););
+  const dim3 gr(nblk(M, 4)), b(256);
+  switch (d) {
+    case 1024: F5H_OP_DISPATCH(compute, T, hipLaunchKernelGGL((rms_kernel<T, 4>), gr, b, 0, st, h, M, d, g, (T*)out);); break;
+    case 512: F5H_OP_DISPATCH(compute, T, hipLaunchKernelGGL((rms_kernel<T, 2>), gr, b, 0, st, h, M, d, g, (T*)out);); break;
+    default: F5H_OP_DISPATCH(compute, T, hipLaunchKernelGGL((rms_kernel<T, 0>), gr, b, 0, st, h, M, d, g, (T*)out););
+  }
   return hipGetLastError();
 }
 

@@ -16,6 +16,9 @@ SHAPES = {  # name: (M, N, K); C2 = 2 x 1876 rows, C3 = 64 x 1876 rows
     "c2_qkv": (3752, 3072, 1024), "c2_ffn1": (3752, 2048, 1024), "c2_out": (3752, 1024, 1024),
     "c2_ffn2": (3752, 1024, 2048), "c3_qkv": (120064, 3072, 1024), "c3_ffn2": (120064, 1024, 2048),
 }
+for _k in (128, 256, 512, 2048, 4096):  # K sweeps at the C2 output shapes: fixed cost per launch = intercept
+    SHAPES[f"c2_out_k{_k}"] = (3752, 1024, _k)
+    SHAPES[f"c2_qkv_k{_k}"] = (3752, 3072, _k)
 CFGS = {0: (64, 128, 256), 1: (128, 128, 256), 5: (192, 128, 256), 11: (256, 256, 512)}
 # round 2 also timed 8-wave one-block-per-CU tiles (128x256, 192x256, 256x128, 128x128, 256x256, 256x192),
 # K32-stage deep rings (64x128..128x256) and DMA issue interleaved with the MFMAs; all slower at C2
@@ -32,6 +35,10 @@ def grid_threads(M, N, cfg):
     return ((M + bm - 1) // bm) * ((N + bn - 1) // bn) * th
 
 
+ROUNDS, PER = 5, REPS // 5  # interleaved rounds per shape (MI355X_MICROARCH DVFS: compare within one process)
+MODES = [-1]  # round 2 also A/B'd a tile -> XCD rectangle grouping here: no gain (profiles/r02_gemm_tune_c2_xcd.txt)
+
+
 def run():
     import torch
     from f5_tts_amd.engine import gemm_force_config, op_linear
@@ -40,32 +47,40 @@ def run():
     for name, (M, N, K) in SHAPES.items():
         A = torch.randn(M, K, device=dev)
         W = torch.randn(N, K, device=dev) / K ** 0.5
-        for cfg in CFGS:
-            gemm_force_config(cfg)
-            for _ in range(REPS):
-                op_linear(A, W, None, compute="bf16")
+        for _ in range(ROUNDS):
+            for cfg in CFGS:
+                gemm_force_config(cfg)
+                for mode in MODES:
+                    for _ in range(PER):
+                        op_linear(A, W, None, compute="bf16")
         torch.cuda.synchronize()
         print(f"done {name}", flush=True)
     gemm_force_config(-1)
 
 
 def report(path):
-    """The gemm dispatches in issue order are SHAPES x CFGS x REPS (run() order)."""
+    """The gemm dispatches in issue order are SHAPES x ROUNDS x CFGS x MODES x PER (run() order)."""
     rows = sorted(csv.DictReader(open(path)), key=lambda r: int(r["Start_Timestamp"]))
     ts = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3 for r in rows
           if "gemm_" in r["Kernel_Name"]]
-    assert len(ts) == len(SHAPES) * len(CFGS) * REPS, len(ts)
+    assert len(ts) == len(SHAPES) * ROUNDS * len(CFGS) * len(MODES) * PER, len(ts)
     k = 0
     for name, (M, N, K) in SHAPES.items():
+        got = {}
+        for _ in range(ROUNDS):
+            for cfg in CFGS:
+                for mode in MODES:
+                    got.setdefault((cfg, mode), []).extend(ts[k:k + PER])
+                    k += PER
         line = []
-        for cfg in CFGS:
-            t = sorted(ts[k:k + REPS])[: REPS * 3 // 4]  # drop the slowest quarter (cold caches)
-            k += REPS
+        for (cfg, mode), t in got.items():
+            t = sorted(t)[: len(t) * 3 // 4]  # drop the slowest quarter (cold caches)
             avg = sum(t) / len(t)
-            line.append(f"cfg{cfg:<2d} {avg:8.2f}us {2 * M * N * K / avg / 1e6:5.0f}TF")
+            tag = f"cfg{cfg}" + (f"/x{mode}" if len(MODES) > 1 else "")
+            line.append(f"{tag:9s} {avg:8.2f}us {2 * M * N * K / avg / 1e6:5.0f}TF")
         print(f"{name:8s}")
-        for i in range(0, len(line), 8):
-            print("   " + " | ".join(line[i:i + 8]))
+        for i in range(0, len(line), 6):
+            print("   " + " | ".join(line[i:i + 6]))
 
 
 if __name__ == "__main__":
