@@ -29,6 +29,17 @@ def compute_for_dtype(dtype: torch.dtype) -> str:
     return "fp32"
 
 
+# bumped whenever any module in the process registers a submodule (torch's global registration hook)
+_STRUCT_GEN = [0]
+
+
+def _bump_struct_gen(module, name, submodule):
+    _STRUCT_GEN[0] += 1
+
+
+torch.nn.modules.module.register_module_module_registration_hook(_bump_struct_gen)
+
+
 class EngineBackbone(nn.Module):
     backbone_name = "DiT"
 
@@ -47,8 +58,16 @@ class EngineBackbone(nn.Module):
     # ------------------------------------------------------------------ engine cache
     def _weights_version(self):
         # _version misses writes through .data (p.data.copy_); the storage pointer and dtype catch
-        # re-assigned / re-cast parameters, so a stale packed engine is never reused
-        return tuple((p._version, p.data_ptr(), p.dtype) for p in self.parameters()) + (id(self),)
+        # re-assigned / re-cast parameters, so a stale packed engine is never reused. The module list
+        # is cached (walking the ~300-module tree per call cost ~1 ms of host time) and rebuilt when
+        # any module registers a submodule; each module's own parameter dict is read every call, so a
+        # replaced Parameter object is seen too.
+        mods = self.__dict__.get("_mods")
+        if mods is None or mods[0] != _STRUCT_GEN[0]:
+            mods = (_STRUCT_GEN[0], tuple(self.modules()))
+            self.__dict__["_mods"] = mods
+        return tuple((p._version, p.data_ptr(), p.dtype) for m in mods[1] for p in m._parameters.values()
+                     if p is not None) + (id(self),)
 
     def engine_weights(self) -> dict:
         return {k: v for k, v in self.state_dict().items() if not k.endswith("inv_freq")}
@@ -77,9 +96,10 @@ class EngineBackbone(nn.Module):
         import copy
 
         for k, v in self.__dict__.items():
-            if k in ("_engines", "_engine_lock"):
+            if k in ("_engines", "_engine_lock", "_mods"):
                 continue
             new.__dict__[k] = copy.deepcopy(v, memo)
+        new.__dict__.pop("_mods", None)
         new.__dict__["_engines"] = {}
         new.__dict__["_engine_lock"] = threading.Lock()
         return new

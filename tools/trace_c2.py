@@ -56,14 +56,24 @@ def report(path, calls=3):
     per = defaultdict(list)
     busy_end = t0
     idle = 0
+    gaps = []
+    prev = win[0]["Kernel_Name"]
     for r in win:
         s, e = int(r["Start_Timestamp"]), int(r["End_Timestamp"])
         per[r["Kernel_Name"].split("(")[0][:90]].append((e - s) / 1e3)
         if s > busy_end:
             idle += s - busy_end
+            gaps.append(((s - busy_end) / 1e3, prev.split("(")[0][:50], r["Kernel_Name"].split("(")[0][:50]))
         busy_end = max(busy_end, e)
+        prev = r["Kernel_Name"]
     print(f"window {span:.1f} us for {calls} calls = {span / calls:.1f} us/call; idle gaps {idle / 1e3:.1f} us "
           f"({idle / 1e3 / span * 100:.1f} %), {len(win)} dispatches")
+    big = sorted(gaps, reverse=True)
+    small = [g for g in gaps if g[0] < 5.0]
+    print(f"gaps: {len(gaps)}; < 5 us: {len(small)} totalling {sum(g[0] for g in small):.1f} us; "
+          f">= 5 us: {len(gaps) - len(small)} totalling {sum(g[0] for g in gaps) - sum(g[0] for g in small):.1f} us")
+    for g in big[:12]:
+        print(f"   gap {g[0]:8.1f} us  after {g[1]}  before {g[2]}")
     tot = sum(sum(v) for v in per.values())
     for name, v in sorted(per.items(), key=lambda kv: -sum(kv[1])):
         print(f"{sum(v) / tot * 100:5.1f}%  n={len(v) // calls:5d}/call  avg {sum(v) / len(v):8.2f} us  {name}")
