@@ -1,16 +1,55 @@
 // ConvPositionEmbedding (modules.py:175-201): Conv1d(d, d, k=31, groups=16, pad=15) [+mask] -> Mish,
-// as an implicit GEMM on MFMA. One workgroup = 64 positions x the 64 output channels of one
-// group of one sequence; K = 31 taps x 64 input channels. The input window (94 rows x 64 ch)
-// is staged once in LDS (masked rows -> 0); the 31 weight taps stream through a
-// double-buffered LDS panel, TS taps per stage (bf16: 4, so 8 barriers per block instead of 31;
-// fp32: 1). Same k-slab MFMA scheme as the GEMM (bf16 16x16x32 / fp32 16x16x4).
+// as an implicit GEMM on MFMA: K = 31 taps x 64 input channels of one group.
+//
+// 16-bit operands (conv16_kernel): one workgroup = 256 positions x the 64 output channels of one
+// group of one sequence (C2: 8 x 16 x 2 = 256 workgroups, one round on 256 CUs), 8 waves as
+// 4 (positions) x 2 (channels), 64 x 32 outputs per wave. The input window (286 rows x 64 ch) is
+// staged once in LDS (masked rows -> 0); the group's 31 weight taps (254 KB) stream through a
+// 3-slot LDS-DMA ring, 4 taps per slot, one stage kept in flight across each barrier (counted
+// vmcnt, raw s_barrier), so each weight byte read from L2 serves 256 positions.
+// fp32 parity operands (conv_kernel): 64 positions per workgroup, one tap per stage.
+// Same k-slab MFMA scheme as the GEMM (bf16/fp16 16x16x32, fp32 16x16x4).
 #include "common.h"
 #include "kernels.h"
 
 namespace f5h {
 
-// NWM x 2 waves; block = 32*NWM positions x 64 output channels (NWM = 4: 128 positions, so each
-// 254 KB group weight stream from L2 serves twice the outputs of the 64-position block)
+// Mish epilogue of one 8-channel row chunk (shared by both kernels): bias, row mask, Mish, then the
+// operand-dtype store (mode 0) or the fp32 store with the residual added (mode 1).
+template <typename TC>
+F5H_DEV void conv_epi8(const ConvArgs& a, const float* c, int s, int pos, int oc, bool keep) {
+  const int d = a.d;
+  float v[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const float x = keep ? c[e] + a.bias[oc + e] : 0.f;
+    v[e] = is16<TC>() ? mish_fast(x) : mish(x);
+  }
+  if (a.mode == 0) {
+    TC* y = reinterpret_cast<TC*>(a.y) + ((int64_t)s * a.L + pos) * d + oc;
+    if constexpr (is16<TC>()) {
+      typename Op16<TC>::v8 o = {from_f32<TC>(v[0]), from_f32<TC>(v[1]), from_f32<TC>(v[2]), from_f32<TC>(v[3]),
+                                 from_f32<TC>(v[4]), from_f32<TC>(v[5]), from_f32<TC>(v[6]), from_f32<TC>(v[7])};
+      *reinterpret_cast<typename Op16<TC>::v8*>(y) = o;
+    } else {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) y[e] = from_f32<TC>(v[e]);
+    }
+  } else {
+    float* y = reinterpret_cast<float*>(a.y) + ((int64_t)s * a.y_seq_stride + a.y_row_off + pos) * d + oc;
+    const float* rs = a.resid + ((int64_t)s * a.L + pos) * d + oc;
+    const float4 r0 = *reinterpret_cast<const float4*>(rs), r1 = *reinterpret_cast<const float4*>(rs + 4);
+    *reinterpret_cast<float4*>(y) = make_float4(v[0] + r0.x, v[1] + r0.y, v[2] + r0.z, v[3] + r0.w);
+    *reinterpret_cast<float4*>(y + 4) = make_float4(v[4] + r1.x, v[5] + r1.y, v[6] + r1.z, v[7] + r1.w);
+  }
+}
+
+template <int N>
+F5H_DEV void wait_vm() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"i"(N) : "memory");
+}
+
+// fp32 parity path: NWM x 2 waves; block = 32*NWM positions x 64 output channels, one tap per stage.
 template <typename TC, typename TX, int NWM = 2>
 __global__ __launch_bounds__(128 * NWM, 1) void conv_kernel(ConvArgs a) {
   constexpr int E = elems16<TC>();
@@ -130,31 +169,135 @@ __global__ __launch_bounds__(128 * NWM, 1) void conv_kernel(ConvArgs a) {
   for (int c = tid; c < BP * 8; c += NT) {
     const int row = c >> 3, c8 = (c & 7) * 8, pos = n0 + row;
     if (pos >= L || c8 >= cg) continue;
-    const int oc = grp * cg + c8;
     const bool keep = !a.rowkeep || a.rowkeep[(int64_t)s * L + pos];
-    float v[8];
+    conv_epi8<TC>(a, Cs + row * CP + c8, s, pos, grp * cg + c8, keep);
+  }
+}
+
+template <typename TC, typename TX>
+__global__ __launch_bounds__(512, 1) void conv16_kernel(ConvArgs a) {
+  constexpr int CPR = 8;                  // 16-B chunks per 64-channel row
+  constexpr int BP = 256, NT = 512;       // positions per block, threads
+  constexpr int WROWS = BP + 30;          // input window rows
+  constexpr int TS = 4, NST = 8, RING = 3;  // taps per stage, stages (31 taps), ring slots
+  constexpr int TAPB = 64 * CPR;          // uint4 per tap panel (64 out ch x 64 in ch)
+  typedef typename Slab<TC>::frag frag;
+  __shared__ __attribute__((aligned(16))) uint4 lds[WROWS * CPR + RING * TS * TAPB];
+  uint4* Xs = lds;
+  uint4* Ws0 = lds + WROWS * CPR;
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid >> 1, wn = wid & 1;  // 4 x 64 positions, 2 x 32 channels
+  const int n0 = blockIdx.x * BP, grp = blockIdx.y, s = blockIdx.z;
+  const int L = a.L, d = a.d;
+  const TX* X = reinterpret_cast<const TX*>(a.x);
+  const int cg = d / 16;  // channels per group (<= 64; padded to 64 in LDS and in the packed weights)
+  const TC* Wg = reinterpret_cast<const TC*>(a.w) + (int64_t)grp * 31 * 64 * 64;
+
+  // window rows q = n0-15 .. n0+270, plain loads (drained before the weight DMA is issued)
+  for (int idx = tid; idx < WROWS * CPR; idx += NT) {
+    const int row = idx / CPR, ch = idx % CPR;
+    const int q = n0 - 15 + row;
+    const bool ok = q >= 0 && q < L && ch * 8 < cg && (!a.rowkeep || a.rowkeep[(int64_t)s * L + q]);
+    const TX* src = X + ((int64_t)s * L + (ok ? q : 0)) * d + grp * cg + (ok ? ch * 8 : 0);
+    Xs[row * CPR + swz128(row, ch)] = Load16<TC, TX>::ld(src, ok);
+  }
+  // tap panel: lane chunk p = wid*64 + lane -> row p/8, source chunk swz128(row, p%8) (involution)
+  const int prow = (wid * 64 + lane) / CPR, pslot = (wid * 64 + lane) % CPR;
+  const int woff = prow * 64 + swz128(prow, pslot) * 8;
+  auto wdma = [&](int st) {  // stage st -> ring slot st % RING; one 1 KB piece per tap per wave
+    uint4* Wslot = Ws0 + (st % RING) * TS * TAPB;
 #pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      float x = keep ? Cs[row * CP + c8 + e] + a.bias[oc + e] : 0.f;
-      v[e] = is16<TC>() ? mish_fast(x) : mish(x);
+    for (int u = 0; u < TS; ++u) {
+      const int t = st * TS + u;
+      if (t < 31)
+        __builtin_amdgcn_global_load_lds((const void*)(Wg + (int64_t)t * 64 * 64 + woff),
+                                         (LDS_PTR(void))(Wslot + u * TAPB + wid * 64), 16, 0, 0);
     }
-    if (a.mode == 0) {
-      TC* y = reinterpret_cast<TC*>(a.y) + ((int64_t)s * L + pos) * d + oc;
-      if constexpr (is16<TC>()) {
-        typename Op16<TC>::v8 o = {from_f32<TC>(v[0]), from_f32<TC>(v[1]), from_f32<TC>(v[2]), from_f32<TC>(v[3]),
-                                   from_f32<TC>(v[4]), from_f32<TC>(v[5]), from_f32<TC>(v[6]), from_f32<TC>(v[7])};
-        *reinterpret_cast<typename Op16<TC>::v8*>(y) = o;
-      } else {
+  };
+  auto taps_of = [](int st) { return st < 0 || st >= NST ? 0 : (31 - st * TS < TS ? 31 - st * TS : TS); };
+  // wait until stage `st` has landed given stages up to `issued` were issued (younger stay in flight)
+  auto wait_stage = [&](int st, int issued) {
+    int younger = 0;
+    for (int k = st + 1; k <= issued; ++k) younger += taps_of(k);
+    switch (younger) {
+      case 0: wait_vm<0>(); break;
+      case 3: wait_vm<3>(); break;
+      case 4: wait_vm<4>(); break;
+      case 7: wait_vm<7>(); break;
+      default: wait_vm<8>(); break;
+    }
+  };
+
+  f32x4 acc[4][2];
 #pragma unroll
-        for (int e = 0; e < 8; ++e) y[e] = from_f32<TC>(v[e]);
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");  // window in LDS (own part)
+  for (int st = 0; st < RING; ++st) wdma(st);
+  wait_stage(0, RING - 1);
+  __builtin_amdgcn_s_barrier();  // window + stage 0 visible to every wave
+  for (int st = 0; st < NST; ++st) {
+    const uint4* Wslot = Ws0 + (st % RING) * TS * TAPB;
+#pragma unroll
+    for (int u = 0; u < TS; ++u) {
+      const int t = st * TS + u;
+      if (t < 31) {
+        const uint4* Ws = Wslot + u * TAPB;
+        frag af[2][4], bfr[2][2];
+#pragma unroll
+        for (int sl = 0; sl < 2; ++sl) {
+          const int ch = sl * 4 + (lane >> 4);
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const int row = wm * 64 + i * 16 + (lane & 15) + t;  // window row of input pos + t - 15
+            af[sl][i] = __builtin_bit_cast(frag, Xs[row * CPR + swz128(row, ch)]);
+          }
+#pragma unroll
+          for (int j = 0; j < 2; ++j) {
+            const int row = wn * 32 + j * 16 + (lane & 15);
+            bfr[sl][j] = __builtin_bit_cast(frag, Ws[row * CPR + swz128(row, ch)]);
+          }
+        }
+#pragma unroll
+        for (int sl = 0; sl < 2; ++sl)
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < 2; ++j) acc[i][j] = Slab<TC>::mma(af[sl][i], bfr[sl][j], acc[i][j]);
       }
-    } else {
-      float* y = reinterpret_cast<float*>(a.y) + ((int64_t)s * a.y_seq_stride + a.y_row_off + pos) * d + oc;
-      const float* rs = a.resid + ((int64_t)s * L + pos) * d + oc;
-      const float4 r0 = *reinterpret_cast<const float4*>(rs), r1 = *reinterpret_cast<const float4*>(rs + 4);
-      *reinterpret_cast<float4*>(y) = make_float4(v[0] + r0.x, v[1] + r0.y, v[2] + r0.z, v[3] + r0.w);
-      *reinterpret_cast<float4*>(y + 4) = make_float4(v[4] + r1.x, v[5] + r1.y, v[6] + r1.z, v[7] + r1.w);
     }
+    if (st + 1 < NST) {
+      // stage st+1 landed (own pieces) -> barrier publishes it and retires every wave's reads of
+      // slot st % RING, which stage st + RING then refills
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      wait_stage(st + 1, st + RING - 1 < NST ? st + RING - 1 : NST - 1);
+      __builtin_amdgcn_s_barrier();
+      if (st + RING < NST) wdma(st + RING);
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+  __syncthreads();
+
+  // epilogue through LDS: [BP][68] fp32 image, 8-channel row chunks
+  constexpr int CP = 68;
+  static_assert(BP * CP * 4 <= (int)sizeof(lds), "epilogue tile fits the LDS image");
+  float* Cs = reinterpret_cast<float*>(lds);
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        Cs[(wm * 64 + i * 16 + (lane >> 4) * 4 + r) * CP + wn * 32 + j * 16 + (lane & 15)] = acc[i][j][r];
+  __syncthreads();
+  for (int c = tid; c < BP * 8; c += NT) {
+    const int row = c >> 3, c8 = (c & 7) * 8, pos = n0 + row;
+    if (pos >= L || c8 >= cg) continue;
+    const bool keep = !a.rowkeep || a.rowkeep[(int64_t)s * L + pos];
+    conv_epi8<TC>(a, Cs + row * CP + c8, s, pos, grp * cg + c8, keep);
   }
 }
 
@@ -162,17 +305,17 @@ hipError_t conv_pos(int compute, const ConvArgs& a, hipStream_t st) {
   // groups = 16; d/16 channels per group, padded to the 64-channel tile (d % 128 == 0)
   if (a.d % 128 != 0 || a.d > 1024) return hipErrorInvalidValue;
   if (compute == F5H_C_BF16 || compute == F5H_C_FP16) {
-    dim3 grid((a.L + 127) / 128, 16, a.S);
+    dim3 grid((a.L + 255) / 256, 16, a.S);
     if (compute == F5H_C_BF16) {
       if (a.x_f32)
-        hipLaunchKernelGGL((conv_kernel<bf16, float, 4>), grid, dim3(512), 0, st, a);
+        hipLaunchKernelGGL((conv16_kernel<bf16, float>), grid, dim3(512), 0, st, a);
       else
-        hipLaunchKernelGGL((conv_kernel<bf16, bf16, 4>), grid, dim3(512), 0, st, a);
+        hipLaunchKernelGGL((conv16_kernel<bf16, bf16>), grid, dim3(512), 0, st, a);
     } else {
       if (a.x_f32)
-        hipLaunchKernelGGL((conv_kernel<f16, float, 4>), grid, dim3(512), 0, st, a);
+        hipLaunchKernelGGL((conv16_kernel<f16, float>), grid, dim3(512), 0, st, a);
       else
-        hipLaunchKernelGGL((conv_kernel<f16, f16, 4>), grid, dim3(512), 0, st, a);
+        hipLaunchKernelGGL((conv16_kernel<f16, f16>), grid, dim3(512), 0, st, a);
     }
   } else {
     dim3 grid((a.L + 63) / 64, 16, a.S);
