@@ -174,6 +174,22 @@ __global__ __launch_bounds__(128 * NWM, 1) void conv_kernel(ConvArgs a) {
   }
 }
 
+// Input-window image: fragment reads take rows t + 16i + (lane & 15) for every tap t, so the
+// conflict-free swizzle must hold for every row offset: chunk c of row r at c ^ (2 * ((r >> 1) & 3))
+// covers each (row parity, 16-B slot) pair once per ds_read_b128 lane group at any offset (the
+// weight panels use the GEMM's swz128g). Checked against the lane groups of MI355X_MICROARCH.md.
+template <int OFF>
+F5H_DEV u32x4 lds_rd128(uint32_t addr) {  // ds_read_b128 hidden from hipcc's waitcnt bookkeeping
+  u32x4 r;
+  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(r) : "v"(addr), "i"(OFF));
+  return r;
+}
+F5H_DEV int swz_win(int row, int chunk) { return chunk ^ (((row >> 1) & 3) << 1); }
+F5H_DEV int swz_tap(int row, int chunk) {
+  const int r = row & 15;
+  return chunk ^ ((r >> 1) ^ ((unsigned)(r - 4) < 8u ? 1 : 0));
+}
+
 template <typename TC, typename TX>
 __global__ __launch_bounds__(512, 1) void conv16_kernel(ConvArgs a) {
   constexpr int CPR = 8;                  // 16-B chunks per 64-channel row
@@ -194,17 +210,50 @@ __global__ __launch_bounds__(512, 1) void conv16_kernel(ConvArgs a) {
   const int cg = d / 16;  // channels per group (<= 64; padded to 64 in LDS and in the packed weights)
   const TC* Wg = reinterpret_cast<const TC*>(a.w) + (int64_t)grp * 31 * 64 * 64;
 
-  // window rows q = n0-15 .. n0+270, plain loads (drained before the weight DMA is issued)
-  for (int idx = tid; idx < WROWS * CPR; idx += NT) {
-    const int row = idx / CPR, ch = idx % CPR;
-    const int q = n0 - 15 + row;
-    const bool ok = q >= 0 && q < L && ch * 8 < cg && (!a.rowkeep || a.rowkeep[(int64_t)s * L + q]);
-    const TX* src = X + ((int64_t)s * L + (ok ? q : 0)) * d + grp * cg + (ok ? ch * 8 : 0);
-    Xs[row * CPR + swz128(row, ch)] = Load16<TC, TX>::ld(src, ok);
+  // window rows q = n0-15 .. n0+270, plain loads (drained before the weight DMA is issued). Every
+  // thread issues all of its loads before converting any (addresses clamped in range, so no load
+  // waits on the row mask): one memory round trip instead of one per 512-chunk pass.
+  {
+    constexpr int NIT = (WROWS * CPR + NT - 1) / NT;
+    constexpr int EPC = 16 / sizeof(TX);  // TX elements per 16-B load; 8 channels = 1 (16-bit) or 2 (fp32) loads
+    uint4 raw[NIT][8 / EPC];
+    bool okv[NIT];
+#pragma unroll
+    for (int it = 0; it < NIT; ++it) {
+      const int idx = tid + it * NT, row = idx / CPR, ch = idx % CPR;
+      const int q = n0 - 15 + row;
+      const int qc = min(max(q, 0), L - 1), cc = ch * 8 < cg ? ch * 8 : 0;
+      okv[it] = idx < WROWS * CPR && q >= 0 && q < L && ch * 8 < cg;
+      const uint4* src = reinterpret_cast<const uint4*>(X + ((int64_t)s * L + qc) * d + grp * cg + cc);
+#pragma unroll
+      for (int h = 0; h < 8 / EPC; ++h) raw[it][h] = idx < WROWS * CPR ? src[h] : make_uint4(0, 0, 0, 0);
+    }
+    if (a.rowkeep) {
+#pragma unroll
+      for (int it = 0; it < NIT; ++it) {
+        const int idx = tid + it * NT, q = n0 - 15 + idx / CPR;
+        if (okv[it]) okv[it] = a.rowkeep[(int64_t)s * L + q] != 0;
+      }
+    }
+#pragma unroll
+    for (int it = 0; it < NIT; ++it) {
+      const int idx = tid + it * NT, row = idx / CPR, ch = idx % CPR;
+      if (idx >= WROWS * CPR) continue;
+      uint4 v;
+      if constexpr (EPC == 8) {
+        v = raw[it][0];
+      } else {
+        const float4 x0 = __builtin_bit_cast(float4, raw[it][0]), x1 = __builtin_bit_cast(float4, raw[it][1]);
+        typename Op16<TC>::v8 o = {from_f32<TC>(x0.x), from_f32<TC>(x0.y), from_f32<TC>(x0.z), from_f32<TC>(x0.w),
+                                   from_f32<TC>(x1.x), from_f32<TC>(x1.y), from_f32<TC>(x1.z), from_f32<TC>(x1.w)};
+        v = __builtin_bit_cast(uint4, o);
+      }
+      Xs[row * CPR + swz_win(row, ch)] = okv[it] ? v : make_uint4(0, 0, 0, 0);
+    }
   }
-  // tap panel: lane chunk p = wid*64 + lane -> row p/8, source chunk swz128(row, p%8) (involution)
+  // tap panel: lane chunk p = wid*64 + lane -> row p/8, source chunk swz_tap(row, p%8) (involution)
   const int prow = (wid * 64 + lane) / CPR, pslot = (wid * 64 + lane) % CPR;
-  const int woff = prow * 64 + swz128(prow, pslot) * 8;
+  const int woff = prow * 64 + swz_tap(prow, pslot) * 8;
   auto wdma = [&](int st) {  // stage st -> ring slot st % RING; one 1 KB piece per tap per wave
     uint4* Wslot = Ws0 + (st % RING) * TS * TAPB;
 #pragma unroll
@@ -239,36 +288,68 @@ __global__ __launch_bounds__(512, 1) void conv16_kernel(ConvArgs a) {
   for (int st = 0; st < RING; ++st) wdma(st);
   wait_stage(0, RING - 1);
   __builtin_amdgcn_s_barrier();  // window + stage 0 visible to every wave
-  for (int st = 0; st < NST; ++st) {
-    const uint4* Wslot = Ws0 + (st % RING) * TS * TAPB;
+
+  // Fragment reads are inline asm (invisible to hipcc's waitcnt bookkeeping), two register sets: the
+  // 12 reads of tap t+1 are in flight while tap t's 16 MFMAs run (the first tap of a stage waits for
+  // the stage barrier). Window rows for tap t: r0 + 16 i + t; the swizzle depends on (r0 + t) only.
+  const uint32_t lds0 = (uint32_t)(uintptr_t)(LDS_PTR(void))lds;
+  const int q = lane >> 4, r0 = wm * 64 + (lane & 15);
+  uint32_t bbase[2];
 #pragma unroll
-    for (int u = 0; u < TS; ++u) {
+  for (int sl = 0; sl < 2; ++sl) {
+    const int row = wn * 32 + (lane & 15);
+    bbase[sl] = lds0 + (uint32_t)(WROWS * CPR * 16) + row * 128 + swz_tap(row, sl * 4 + q) * 16;
+  }
+  typedef u32x4 FR[12];  // [0..7]: A (slab, i); [8..11]: B (slab, j)
+  auto rd = [&](int t, FR& f) {
+    const int rt = r0 + t, st = t / TS, u = t - st * TS;
+    const uint32_t wo = (uint32_t)(((st % RING) * TS + u) * TAPB * 16);
+    static_for<0, 2>([&](auto SL) {
+      constexpr int sl = decltype(SL)::value;
+      const uint32_t ab = lds0 + rt * 128 + swz_win(rt, sl * 4 + q) * 16;
+      static_for<0, 4>([&](auto I) {
+        constexpr int i = decltype(I)::value;
+        f[sl * 4 + i] = lds_rd128<i * 16 * 128>(ab);
+      });
+      static_for<0, 2>([&](auto J) {
+        constexpr int j = decltype(J)::value;
+        f[8 + sl * 2 + j] = lds_rd128<j * 16 * 128>(bbase[sl] + wo);
+      });
+    });
+  };
+  auto mm = [&](FR& f) {
+#pragma unroll
+    for (int k = 0; k < 12; ++k) asm volatile("" : "+v"(f[k]));
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int sl = 0; sl < 2; ++sl)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[i][j] = Slab<TC>::mma(__builtin_bit_cast(frag, f[sl * 4 + i]), __builtin_bit_cast(frag, f[8 + sl * 2 + j]),
+                                    acc[i][j]);
+    __builtin_amdgcn_sched_barrier(0);
+  };
+  FR fa, fb;
+  rd(0, fa);
+  for (int st = 0; st < NST; ++st) {
+    // taps st*TS .. : even taps in fa, odd in fb (TS is even); tap t+1 is prefetched inside the stage
+    static_for<0, TS>([&](auto U) {
+      constexpr int u = decltype(U)::value;
       const int t = st * TS + u;
       if (t < 31) {
-        const uint4* Ws = Wslot + u * TAPB;
-        frag af[2][4], bfr[2][2];
-#pragma unroll
-        for (int sl = 0; sl < 2; ++sl) {
-          const int ch = sl * 4 + (lane >> 4);
-#pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            const int row = wm * 64 + i * 16 + (lane & 15) + t;  // window row of input pos + t - 15
-            af[sl][i] = __builtin_bit_cast(frag, Xs[row * CPR + swz128(row, ch)]);
-          }
-#pragma unroll
-          for (int j = 0; j < 2; ++j) {
-            const int row = wn * 32 + j * 16 + (lane & 15);
-            bfr[sl][j] = __builtin_bit_cast(frag, Ws[row * CPR + swz128(row, ch)]);
-          }
+        FR& cur = (u & 1) ? fb : fa;
+        FR& nxt = (u & 1) ? fa : fb;
+        if (u + 1 < TS && t + 1 < 31) {
+          rd(t + 1, nxt);
+          asm volatile("s_waitcnt lgkmcnt(12)" ::: "memory");
+        } else {
+          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         }
-#pragma unroll
-        for (int sl = 0; sl < 2; ++sl)
-#pragma unroll
-          for (int i = 0; i < 4; ++i)
-#pragma unroll
-            for (int j = 0; j < 2; ++j) acc[i][j] = Slab<TC>::mma(af[sl][i], bfr[sl][j], acc[i][j]);
+        mm(cur);
       }
-    }
+    });
     if (st + 1 < NST) {
       // stage st+1 landed (own pieces) -> barrier publishes it and retires every wave's reads of
       // slot st % RING, which stage st + RING then refills
@@ -276,6 +357,7 @@ __global__ __launch_bounds__(512, 1) void conv16_kernel(ConvArgs a) {
       wait_stage(st + 1, st + RING - 1 < NST ? st + RING - 1 : NST - 1);
       __builtin_amdgcn_s_barrier();
       if (st + RING < NST) wdma(st + RING);
+      rd((st + 1) * TS, fa);
     }
   }
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
