@@ -13,6 +13,9 @@
 //     (cdna_hip_programming.md T13; the branch is forced by the spike tests).
 //   * row sums on the matrix pipe: l^T += ones . P^T (4 extra MFMAs per tile instead of 32 VALU
 //     adds), summed from the same 16-bit P that enters O.
+//   * the QK^T chains start from a loop-carried -m_run block (rewritten only on a re-base), and P
+//     is produced in four 16-key chunks whose MFMAs are issued between the next chunk's exp2s
+//     (sched_group_barrier): on gfx950 only a wave's OWN vector work hides under its MFMAs.
 //   * O^T = V^T . P^T: the S^T accumulators, packed to 16 bit, ARE the B operand; V^T comes from
 //     the LDS tile with ds_read_b64_tr_b16 (hardware transpose).
 //   * K/V tiles of 64 keys by LDS-DMA (global_load_lds) into a 3-deep ring shared by all waves,
@@ -21,9 +24,9 @@
 //   * XCD-aware block mapping: all query blocks of a (sequence, head) share one L2.
 // fp32 parity path: one thread per query row on the VALU (exact fp32).
 //
-// Measured alternatives of round 1 (wave priorities, fixed-offset softmax, software-pipelined
-// and 4-wave forms) were parity-tested and none beat this schedule; they were
-// removed from the product library (git history: commit e5075c7).
+// Measured alternatives (rounds 1-2: wave priorities, fixed-offset softmax, software-pipelined,
+// 4-wave, phase-rotated, SIMD ping-pong, deferred-P.V, mid-tile K prefetch, f32 VALU row sums;
+// DESIGN.md §3) were parity-tested and none beat this schedule; they are not in the library.
 #include "common.h"
 #include "kernels.h"
 
@@ -149,12 +152,13 @@ __global__ __launch_bounds__(64 * NW, 1) void attn16_kernel(AttnArgs a) {
   const T one = from_f32<T>(1.f);
   const v8 ones = {one, one, one, one, one, one, one, one};
   float m_run = 0.f;  // running max (log2 units), valid after tile 0
-  f32x16 oacc[2], lacc;
+  f32x16 oacc[2], lacc, minit;  // minit: -m_run in every slot, the QK^T chains' first C operand
 #pragma unroll
   for (int r = 0; r < 16; ++r) {
     oacc[0][r] = 0.f;
     oacc[1][r] = 0.f;
     lacc[r] = 0.f;
+    minit[r] = 0.f;
   }
 
   dma(0, 0);
@@ -195,15 +199,14 @@ __global__ __launch_bounds__(64 * NW, 1) void attn16_kernel(AttnArgs a) {
       });
     };
 
-    // ---- S^T - m_run = K Q^T + (-m_run)
-    const float init = kt == 0 ? 0.f : -m_run;
+    // ---- S^T - m_run = K Q^T + (-m_run): both chains start from minit, which is rewritten only
+    // when m_run changes (no per-tile accumulator initialisation)
     f32x16 sacc[2];
 #pragma unroll
     for (int t = 0; t < 2; ++t) {
+      sacc[t] = OP::mma32(__builtin_bit_cast(v8, kf[t][0]), qf[0], minit);
 #pragma unroll
-      for (int r = 0; r < 16; ++r) sacc[t][r] = init;
-#pragma unroll
-      for (int ks = 0; ks < 4; ++ks) sacc[t] = OP::mma32(__builtin_bit_cast(v8, kf[t][ks]), qf[ks], sacc[t]);
+      for (int ks = 1; ks < 4; ++ks) sacc[t] = OP::mma32(__builtin_bit_cast(v8, kf[t][ks]), qf[ks], sacc[t]);
     }
     vread(std::integral_constant<int, 0>{});
     if (kt * 64 + 64 > klen) {  // ragged last tile: keys past klen get p = 0
@@ -227,6 +230,8 @@ __global__ __launch_bounds__(64 * NW, 1) void attn16_kernel(AttnArgs a) {
       for (int t = 0; t < 2; ++t)
 #pragma unroll
         for (int r = 0; r < 16; ++r) sacc[t][r] -= mx;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) minit[r] = -m_run;
     } else if (!__all(mx <= THR)) {
       // re-base the rows whose scores ran more than THR above m_run (rare: early tiles)
       const float d = fmaxf(mx, 0.f);
@@ -237,29 +242,36 @@ __global__ __launch_bounds__(64 * NW, 1) void attn16_kernel(AttnArgs a) {
         oacc[0][r] *= alpha;
         oacc[1][r] *= alpha;
         lacc[r] *= alpha;
+        minit[r] = -m_run;
       }
 #pragma unroll
       for (int t = 0; t < 2; ++t)
 #pragma unroll
         for (int r = 0; r < 16; ++r) sacc[t][r] -= d;
     }
+    // exp2 / pack of 16-key chunk c = (t, sx) of P, then its three MFMAs (row sums, both O^T
+    // halves), issued between chunk c+1's exp2s and packs: a wave's own VALU work issues in the
+    // shadow of its MFMAs (per accumulator the MFMA order is unchanged)
     v8 pf[2][2];
+    auto exp_chunk = [&](auto C) {
+      constexpr int t = decltype(C)::value >> 1, sx = decltype(C)::value & 1;
 #pragma unroll
-    for (int t = 0; t < 2; ++t)
+      for (int j = 0; j < 8; ++j) pf[t][sx][j] = from_f32<T>(__builtin_amdgcn_exp2f(sacc[t][8 * sx + j]));
+    };
+    auto mma_chunk = [&](auto C) {
+      constexpr int t = decltype(C)::value >> 1, sx = decltype(C)::value & 1;
+      lacc = OP::mma32(ones, pf[t][sx], lacc);  // row sums: l^T += ones . P^T
 #pragma unroll
-      for (int sx = 0; sx < 2; ++sx)
-#pragma unroll
-        for (int j = 0; j < 8; ++j) pf[t][sx][j] = from_f32<T>(__builtin_amdgcn_exp2f(sacc[t][8 * sx + j]));
-
-    asm volatile("s_waitcnt lgkmcnt(7)" ::: "memory");
+      for (int u = 0; u < 2; ++u) {
+        const uint4 w = make_uint4(vf[u][t][sx][0].x, vf[u][t][sx][0].y, vf[u][t][sx][1].x, vf[u][t][sx][1].y);
+        oacc[u] = OP::mma32(__builtin_bit_cast(v8, w), pf[t][sx], oacc[u]);
+      }
+    };
     vread(std::integral_constant<int, 1>{});
-    // row sums: l^T += ones . P^T (any key order)
+    exp_chunk(std::integral_constant<int, 0>{});
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 #pragma unroll
-    for (int t = 0; t < 2; ++t)
-#pragma unroll
-      for (int sx = 0; sx < 2; ++sx) lacc = OP::mma32(ones, pf[t][sx], lacc);
-    auto pv = [&](auto U) {
-      constexpr int u = decltype(U)::value;
+    for (int u = 0; u < 2; ++u)
 #pragma unroll
       for (int t = 0; t < 2; ++t)
 #pragma unroll
@@ -267,20 +279,23 @@ __global__ __launch_bounds__(64 * NW, 1) void attn16_kernel(AttnArgs a) {
           asm volatile("" : "+v"(vf[u][t][sx][0]));
           asm volatile("" : "+v"(vf[u][t][sx][1]));
         }
+    __builtin_amdgcn_sched_barrier(0);
+    static_for<0, 3>([&](auto C) {
+      mma_chunk(C);
+      exp_chunk(std::integral_constant<int, decltype(C)::value + 1>{});
+      // per MFMA gap: 3, 3, 2 exp2 (TRANS) and 1, 1, 2 packs
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x400, 3, 0);
+      __builtin_amdgcn_sched_group_barrier(0x002, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x400, 3, 0);
+      __builtin_amdgcn_sched_group_barrier(0x002, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x400, 2, 0);
+      __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);
       __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-      for (int t = 0; t < 2; ++t)
-#pragma unroll
-        for (int sx = 0; sx < 2; ++sx) {
-          const uint4 w = make_uint4(vf[u][t][sx][0].x, vf[u][t][sx][0].y, vf[u][t][sx][1].x, vf[u][t][sx][1].y);
-          oacc[u] = OP::mma32(__builtin_bit_cast(v8, w), pf[t][sx], oacc[u]);
-        }
-      __builtin_amdgcn_sched_barrier(0);
-    };
-    asm volatile("s_waitcnt lgkmcnt(8)" ::: "memory");
-    pv(std::integral_constant<int, 0>{});
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    pv(std::integral_constant<int, 1>{});
+    });
+    mma_chunk(std::integral_constant<int, 3>{});
   }
   const float l_tot = lacc[0];
   const float inv = l_tot > 0.f ? 1.f / l_tot : 0.f;

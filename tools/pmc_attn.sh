@@ -15,7 +15,7 @@ import csv, statistics, collections
 agg = collections.defaultdict(lambda: collections.defaultdict(list))
 for i in (1, 2):
     for r in csv.DictReader(open(f"gpurun_out/pmc_attn{i}/run_counter_collection.csv")):
-        if "attn_bf16" not in r["Kernel_Name"]:
+        if "attn16" not in r["Kernel_Name"]:
             continue
         k = r["Kernel_Name"].split("(")[0].replace("void ", "")
         agg[k][r["Counter_Name"]].append(float(r["Counter_Value"]))
