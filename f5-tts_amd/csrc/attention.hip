@@ -341,15 +341,27 @@ __global__ __launch_bounds__(64 * NW, 1) void attn16_kernel(AttnArgs a) {
       F5H_A10(5), F5H_A10(6), F5H_A10(7), F5H_A10(8), F5H_A10(9), F5H_A10(10), F5H_A10(11), F5H_A10(12),      \
       F5H_A10(13), F5H_A10(14), F5H_A10(15)
 
-// a[ACC:ACC+15] += A . B, A = arch VGPRs, B = arch VGPRs (P.V and row sums)
-template <typename T, int ACC>
+// a[ACC:ACC+15] += A . B, A = arch VGPRs, B = arch VGPRs (P.V and row sums). PAD: open with the
+// 2 wait states of a just-written A/B operand -- needed wherever hipcc may materialise an operand
+// right before the statement (V^T fragments are assembled by moves, the all-ones row-sum operand
+// is rematerialised from SGPRs under register pressure)
+template <typename T, int ACC, bool PAD>
 F5H_DEV void pw_pv(const typename Op16<T>::v8& A, const typename Op16<T>::v8& B) {
-  if constexpr (std::is_same<T, bf16>::value)
-    asm volatile("s_nop 1\n\tv_mfma_f32_32x32x16_bf16 a[%c2:%c3], %0, %1, a[%c2:%c3]" ::"v"(A), "v"(B), "i"(ACC),
-                 "i"(ACC + 15));
-  else
-    asm volatile("s_nop 1\n\tv_mfma_f32_32x32x16_f16 a[%c2:%c3], %0, %1, a[%c2:%c3]" ::"v"(A), "v"(B), "i"(ACC),
-                 "i"(ACC + 15));
+  if constexpr (PAD) {
+    if constexpr (std::is_same<T, bf16>::value)
+      asm volatile("s_nop 1\n\tv_mfma_f32_32x32x16_bf16 a[%c2:%c3], %0, %1, a[%c2:%c3]" ::"v"(A), "v"(B),
+                   "i"(ACC), "i"(ACC + 15));
+    else
+      asm volatile("s_nop 1\n\tv_mfma_f32_32x32x16_f16 a[%c2:%c3], %0, %1, a[%c2:%c3]" ::"v"(A), "v"(B),
+                   "i"(ACC), "i"(ACC + 15));
+  } else {
+    if constexpr (std::is_same<T, bf16>::value)
+      asm volatile("v_mfma_f32_32x32x16_bf16 a[%c2:%c3], %0, %1, a[%c2:%c3]" ::"v"(A), "v"(B), "i"(ACC),
+                   "i"(ACC + 15));
+    else
+      asm volatile("v_mfma_f32_32x32x16_f16 a[%c2:%c3], %0, %1, a[%c2:%c3]" ::"v"(A), "v"(B), "i"(ACC),
+                   "i"(ACC + 15));
+  }
 }
 // d = K . Q^T + c (first k-step of a score chain), K = a[KA:KA+3], Q = a[QA:QA+3]
 template <typename T, int KA, int QA>
@@ -471,21 +483,21 @@ __global__ __launch_bounds__(256, 1) void attn_pw_kernel(AttnArgs a) {
     const int p = (r * NW + wid) * 64 + lane, row = p >> 3, slot = p & 7;
     dsrc[r] = swz128(row, slot) * 8;
   }
-  // LDS-DMA piece j (0..2*CPW-1: K and V of chunk round j/2) of tile kt into its ring slot; tiles
-  // past the end are clamped re-loads into a dead slot, so every tile issues the same pieces and
-  // the vmcnt arithmetic needs no branch
-  auto dma_piece = [&](int kt, int j) {
-    const int r = j >> 1;
-    uint4* dst = lds + (kt % NS) * (TILE_B / 16) + (j & 1) * 512 + (r * NW + wid) * 64;
+  // K/V tiles are staged through registers: piece j (0..3: K or V of chunk round j/2) of a tile is
+  // one 16-B global load per lane into stg[j] and, a tile later, one ds_write_b128 into the ring
+  // slot. (An LDS-DMA piece costs a wave 100+ issue cycles; these two instructions a few tens.)
+  // Tiles past the end are clamped re-loads into a dead slot, so every tile moves the same pieces.
+  u32x4 stg[2 * CPW];  // (a native vector: HIP's uint4 struct defeats SROA here and lands in scratch)
+  auto gload = [&](int kt, auto J) {
+    constexpr int j = decltype(J)::value, r = j >> 1;
     const int row = ((r * NW + wid) * 64 + lane) >> 3;
     const int64_t off = (int64_t)min(kt * 64 + row, L - 1) * 64 + dsrc[r];
-    __builtin_amdgcn_global_load_lds((const void*)(((j & 1) ? V : K) + off), (LDS_PTR(void))dst, 16, 0, 0);
+    stg[j] = *reinterpret_cast<const u32x4*>(((j & 1) ? V : K) + off);
   };
-  auto dma = [&](int kt) {
-#pragma unroll
-    for (int j = 0; j < 2 * CPW; ++j) dma_piece(kt, j);
+  auto swrite = [&](int kt, auto J) {
+    constexpr int j = decltype(J)::value, r = j >> 1;
+    reinterpret_cast<u32x4*>(lds)[(kt % NS) * (TILE_B / 16) + (j & 1) * 512 + (r * NW + wid) * 64 + lane] = stg[j];
   };
-
   const uint32_t lds0 = (uint32_t)(uintptr_t)(LDS_PTR(void))lds;
   uint32_t kaddr[4];
 #pragma unroll
@@ -536,8 +548,11 @@ __global__ __launch_bounds__(256, 1) void attn_pw_kernel(AttnArgs a) {
 #define PW_LGK(n) asm volatile("s_waitcnt lgkmcnt(%0)" ::"i"(n) : "memory")
 #define PW_VDONE(c) \
   asm volatile("" : "+v"(vf[c][0][0]), "+v"(vf[c][0][1]), "+v"(vf[c][1][0]), "+v"(vf[c][1][1]))
-  // score blocks of group g handed to compiler code: the 16 wait states of an MFMA result
-#define PW_SYNC(g) asm volatile("s_nop 7\n\ts_nop 7" : "+v"(sacc[g][0]), "+v"(sacc[g][1]))
+  // score blocks of group g handed to compiler code after the 12 wait states an (8-pass) MFMA
+  // result needs (PW_SYNC), or as a plain hand-over where more than 12 instructions have issued
+  // since the last MFMA into them (PW_TAKE)
+#define PW_SYNC(g) asm volatile("s_nop 7\n\ts_nop 3" : "+v"(sacc[g][0]), "+v"(sacc[g][1]))
+#define PW_TAKE(g) asm volatile("" : "+v"(sacc[g][0]), "+v"(sacc[g][1]))
 #define PW_FENCE __builtin_amdgcn_sched_barrier(0)
 #ifdef F5H_PW_STAMPS  // diagnostic build: per-phase shader-clock stamps of tile 12 (written over O)
   unsigned long long stamp[8] = {};
@@ -569,11 +584,11 @@ __global__ __launch_bounds__(256, 1) void attn_pw_kernel(AttnArgs a) {
     constexpr int g = decltype(GG)::value;
     constexpr int c = decltype(C)::value, t = c >> 1, sx = c & 1, i = decltype(I)::value;
     if constexpr (i == 0) {
-      pw_pv<T, 48 * g + 32>(ones, pf[g][t][sx]);
+      pw_pv<T, 48 * g + 32, true>(ones, pf[g][t][sx]);
     } else {
       constexpr int u = i - 1;
       const uint4 w = make_uint4(vf[c][u][0].x, vf[c][u][0].y, vf[c][u][1].x, vf[c][u][1].y);
-      pw_pv<T, 48 * g + 16 * u>(__builtin_bit_cast(v8, w), pf[g][t][sx]);
+      pw_pv<T, 48 * g + 16 * u, true>(__builtin_bit_cast(v8, w), pf[g][t][sx]);
     }
   };
   auto smask = [&](auto GG, int kt) {  // ragged last tile: keys past klen get p = 0
@@ -673,11 +688,12 @@ __global__ __launch_bounds__(256, 1) void attn_pw_kernel(AttnArgs a) {
   };
 
   // ---- prologue: tiles 0..2 in flight, K(0) resident, QK^T(A, 0)
-  dma(0);
-  dma(1);
-  dma(2);
-  asm volatile("s_waitcnt vmcnt(%0)" ::"i"(4 * CPW) : "memory");
-  __builtin_amdgcn_s_barrier();
+  for (int t = 0; t < 3; ++t) {
+    static_for<0, 2 * CPW>([&](auto J) { gload(t, J); });
+    static_for<0, 2 * CPW>([&](auto J) { swrite(t, J); });
+  }
+  static_for<0, 2 * CPW>([&](auto J) { gload(3, J); });  // written at the end of beta(0)
+  __syncthreads();
   kread_half(0u, I0{});
   kread_half(0u, I1{});
   PW_LGK(0);
@@ -720,14 +736,12 @@ __global__ __launch_bounds__(256, 1) void attn_pw_kernel(AttnArgs a) {
     });
 
     // ---- beta(kt): MFMA P.V(A, kt), QK^T(A, kt+1) | VALU softmax(B, kt)
-    // tile kt+1 landed (tile kt+2 may stay in flight); the barrier publishes it and retires every
-    // wave's reads of tile kt-1, whose slot tile kt+3 then reuses (its 4 LDS-DMA pieces are issued
-    // between the next MFMAs, where their issue cost overlaps the matrix pipe)
+    // the barrier publishes tile kt+1 (written at the end of beta(kt-2), lgkmcnt(0) since) and
+    // retires every wave's reads of tile kt-1, whose slot tile kt+3 is written at this beta's end
     PW_STAMP(2);
-    asm volatile("s_waitcnt vmcnt(%0)" ::"i"(2 * CPW) : "memory");
     __builtin_amdgcn_s_barrier();
     PW_STAMP(3);
-    PW_SYNC(1);
+    PW_TAKE(1);  // QK^T(B) issued before alpha's 12 P.V MFMAs
     smask(I1{}, kt);
     // LDS reads outstanding: V c0 c1 c2
     PW_LGK(8);
@@ -735,26 +749,21 @@ __global__ __launch_bounds__(256, 1) void attn_pw_kernel(AttnArgs a) {
     vread(so, I3{});  // c1 c2 c3
     PW_FENCE;
     // P.V(A) chunks 0-1 with the row max of B in their shadows (2, 2, 1, 1, 1, 1 pieces)
-    static_assert(2 * CPW == 4, "four DMA pieces per tile and wave");
     pv_one(I0{}, I0{}, I0{});
-    dma_piece(kt + 3, 0);
     smax_part(I1{}, I0{}, m0, m1);
     smax_part(I1{}, I1{}, m0, m1);
     PW_FENCE;
     pv_one(I0{}, I0{}, I1{});
-    dma_piece(kt + 3, 1);
     smax_part(I1{}, I2{}, m0, m1);
     smax_part(I1{}, I3{}, m0, m1);
     PW_FENCE;
     pv_one(I0{}, I0{}, I2{});
-    dma_piece(kt + 3, 2);
     smax_part(I1{}, I4{}, m0, m1);
     PW_LGK(8);
     PW_VDONE(1);
     kread_half(sn, I0{});  // c2 c3 K0 (a[128:143]: QK^T(B, kt) has issued)
     PW_FENCE;
     pv_one(I0{}, I1{}, I0{});
-    dma_piece(kt + 3, 3);
     smax_part(I1{}, std::integral_constant<int, 5>{}, m0, m1);
     PW_FENCE;
     pv_one(I0{}, I1{}, I1{});
@@ -775,12 +784,15 @@ __global__ __launch_bounds__(256, 1) void attn_pw_kernel(AttnArgs a) {
     PW_VDONE(3);
     pv_chunk_exp(I0{}, I3{}, I1{}, I1{});
     PW_STAMP(6);
-    // QK^T(A, kt+1) with B's last exp2s. On the last tile this runs on K(kt) into scores nobody
-    // reads: no branch, so hipcc keeps B's exp2s in the shadows of these MFMAs.
+    // tile kt+3 (loaded during beta(kt-1)) into the slot of tile kt-1
+    static_for<0, 2 * CPW>([&](auto J) { swrite(kt + 3, J); });
+    // QK^T(A, kt+1) with B's last exp2s and the loads of tile kt+4. On the last tile this runs on
+    // K(kt) into scores nobody reads: no branch, so hipcc keeps B's exp2s in the MFMA shadows.
     PW_LGK(0);
     PW_FENCE;
     static_for<0, 8>([&](auto I) {
       constexpr int i = decltype(I)::value;
+      if constexpr (i < 2 * CPW) gload(kt + 4, I);
       qk_one(I0{}, std::integral_constant<int, i / 2>{}, std::integral_constant<int, i % 2>{});
       sexp(I1{}, std::integral_constant<int, 2 + i / 4>{}, std::integral_constant<int, 2 * (i % 4)>{},
            std::integral_constant<int, 2 * (i % 4) + 2>{});
@@ -805,6 +817,7 @@ __global__ __launch_bounds__(256, 1) void attn_pw_kernel(AttnArgs a) {
 #undef PW_LGK
 #undef PW_VDONE
 #undef PW_SYNC
+#undef PW_TAKE
 #undef PW_STAMP
 
   static_for<0, 2>([&](auto GG) {
