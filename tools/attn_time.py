@@ -1,5 +1,4 @@
-"""Times the 16-bit attention kernel at the C2 shape (S=2, H=16, N=1876, q prescaled) for the
-variant selected by F5H_ATTN (0 = 8-wave attn16_kernel, 1 = one-wave-per-SIMD attn_pw_kernel).
+"""Times the 16-bit attention kernel at the C2 shape (S=2, H=16, N=1876, q prescaled).
   rocprofv3 --kernel-trace --stats -d gpurun_out/at -o run -- python tools/attn_time.py
 Also checks the variant against an fp64 softmax of the same rounded operands."""
 import os
@@ -23,5 +22,5 @@ sc = Q.double() @ K.double().transpose(-1, -2)
 p = torch.exp2(sc - sc.amax(-1, keepdim=True))
 ref = ((p / p.sum(-1, keepdim=True)) @ V.double()).transpose(1, 2).reshape(S, N, H * 64)
 err = ((O.cpu().double() - ref).abs().max() / ref.abs().max()).item()
-print(f"F5H_ATTN={os.environ.get('F5H_ATTN', 'default')} N={N} max-rel err {err:.3e}")
+print(f"N={N} max-rel err {err:.3e}")
 assert err < 1e-2
