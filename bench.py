@@ -122,11 +122,17 @@ def class_flops(kc, arch, S, L):
             "conv": 2.0 * S * L * d * (d // 16) * 31}.get(kc, 0.0)
 
 
+def resid_bytes(arch, esz=2):
+    """Width of the residual stream: the operand dtype on the 16-bit DiT path, fp32 otherwise
+    (engine.cpp backbone_part)."""
+    return esz if (esz == 2 and arch["backbone"] == "DiT") else 4
+
+
 def class_bytes(kc, arch, S, L, esz=2):
-    """Algorithmic HBM bytes of one launch of an HBM-bound class: the pre-FFN norm reads the fp32
-    residual rows and writes the 16-bit GEMM operand."""
+    """Algorithmic HBM bytes of one launch of an HBM-bound class: the pre-FFN norm reads the residual
+    rows and writes the 16-bit GEMM operand."""
     if kc == "norm":
-        return S * L * arch["dim"] * (4 + esz)
+        return S * L * arch["dim"] * (resid_bytes(arch, esz) + esz)
     return 0.0
 
 
@@ -159,9 +165,9 @@ def class_entry(kc, avg_ms, n, arch, S, L, launches_per_call, ms_call, chains=1)
     if traffic and kc in ("qkv", "out", "ffn1", "ffn2", "attention"):
         d, ff = arch["dim"], int(arch["dim"] * arch["ff_mult"])
         kn = {"qkv": (d, 3 * d), "out": (d, d), "ffn1": (d, ff), "ffn2": (ff, d)}.get(kc)
-        if kn:  # operands + result at the operand width (fp32 residual read+write for RESID)
+        if kn:  # operands + result at the operand width (residual read+write for RESID)
             K, Nn = kn
-            alg = 2 * (S * L * K + Nn * K) + (8 if kc in ("out", "ffn2") else 2) * S * L * Nn
+            alg = 2 * (S * L * K + Nn * K) + (2 * resid_bytes(arch) if kc in ("out", "ffn2") else 2) * S * L * Nn
         else:
             alg = 4 * 2 * S * arch["heads"] * L * 64
         e["algorithmic_bytes"] = alg

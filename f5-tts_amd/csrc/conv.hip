@@ -15,7 +15,8 @@
 namespace f5h {
 
 // Mish epilogue of one 8-channel row chunk (shared by both kernels): bias, row mask, Mish, then the
-// operand-dtype store (mode 0) or the fp32 store with the residual added (mode 1).
+// operand-dtype store (mode 0), or the residual added in fp32 and stored as fp32 (mode 1) or in the
+// operand dtype (mode 2: the 16-bit residual stream).
 template <typename TC>
 F5H_DEV void conv_epi8(const ConvArgs& a, const float* c, int s, int pos, int oc, bool keep) {
   const int d = a.d;
@@ -34,6 +35,16 @@ F5H_DEV void conv_epi8(const ConvArgs& a, const float* c, int s, int pos, int oc
     } else {
 #pragma unroll
       for (int e = 0; e < 8; ++e) y[e] = from_f32<TC>(v[e]);
+    }
+  } else if (a.mode == 2) {
+    if constexpr (is16<TC>()) {
+      const float* rs = a.resid + ((int64_t)s * a.L + pos) * d + oc;
+      const float4 r0 = *reinterpret_cast<const float4*>(rs), r1 = *reinterpret_cast<const float4*>(rs + 4);
+      TC* y = reinterpret_cast<TC*>(a.y) + ((int64_t)s * a.y_seq_stride + a.y_row_off + pos) * d + oc;
+      typename Op16<TC>::v8 o = {from_f32<TC>(v[0] + r0.x), from_f32<TC>(v[1] + r0.y), from_f32<TC>(v[2] + r0.z),
+                                 from_f32<TC>(v[3] + r0.w), from_f32<TC>(v[4] + r1.x), from_f32<TC>(v[5] + r1.y),
+                                 from_f32<TC>(v[6] + r1.z), from_f32<TC>(v[7] + r1.w)};
+      *reinterpret_cast<typename Op16<TC>::v8*>(y) = o;
     }
   } else {
     float* y = reinterpret_cast<float*>(a.y) + ((int64_t)s * a.y_seq_stride + a.y_row_off + pos) * d + oc;

@@ -152,14 +152,25 @@ F5H_DEV float wave_sum_dpp(float v) {
 
 // LayerNorm(no affine, eps 1e-6) * (1 + scale) + shift (AdaLayerNorm modules.py:325, ff_norm :753,
 // AdaLayerNorm_Final :346). The modulation rows are loaded with the row, before the reductions.
-template <typename TO, int NV>
-__global__ __launch_bounds__(256) void ln_mod_kernel(const float* h, int M, int d, const float* shift,
+// TI: the residual stream's type (fp32, or the operand dtype on the 16-bit DiT path).
+template <typename TI> F5H_DEV float4 load4f(const TI* p);
+template <> F5H_DEV float4 load4f<float>(const float* p) { return *reinterpret_cast<const float4*>(p); }
+template <> F5H_DEV float4 load4f<bf16>(const bf16* p) {
+  const bf16x4 v = *reinterpret_cast<const bf16x4*>(p);
+  return make_float4((float)v[0], (float)v[1], (float)v[2], (float)v[3]);
+}
+template <> F5H_DEV float4 load4f<f16>(const f16* p) {
+  const f16x4 v = *reinterpret_cast<const f16x4*>(p);
+  return make_float4((float)v[0], (float)v[1], (float)v[2], (float)v[3]);
+}
+template <typename TO, int NV, typename TI = float>
+__global__ __launch_bounds__(256) void ln_mod_kernel(const TI* h, int M, int d, const float* shift,
                                                      const float* scale, TO* out) {
   constexpr bool FIXED = NV > 0;
   constexpr int V = FIXED ? NV : MAXV;
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
   if (row >= M) return;
-  const float4* x = reinterpret_cast<const float4*>(h + (int64_t)row * d);
+  const TI* x = h + (int64_t)row * d;
   const float4* sh = reinterpret_cast<const float4*>(shift);
   const float4* sc = reinterpret_cast<const float4*>(scale);
   const int n4 = FIXED ? 64 * NV : d >> 2;
@@ -168,7 +179,7 @@ __global__ __launch_bounds__(256) void ln_mod_kernel(const float* h, int M, int 
   for (int k = 0; k < V; ++k) {
     const int i = lane + 64 * k;
     const bool ok = FIXED || i < n4;
-    v[k] = ok ? x[i] : make_float4(0, 0, 0, 0);
+    v[k] = ok ? load4f<TI>(x + 4 * i) : make_float4(0, 0, 0, 0);
     a[k] = ok ? sc[i] : make_float4(0, 0, 0, 0);
     b[k] = ok ? sh[i] : make_float4(0, 0, 0, 0);
   }
@@ -195,10 +206,29 @@ __global__ __launch_bounds__(256) void ln_mod_kernel(const float* h, int M, int 
                  (v[k].w - mean) * rstd * (1.f + a[k].w) + b[k].w);
   }
 }
-hipError_t ln_modulate(int compute, const float* h, int M, int d, const float* shift, const float* scale, void* out,
-                       hipStream_t st) {
+hipError_t ln_modulate(int compute, const void* hv, int h16, int M, int d, const float* shift, const float* scale,
+                       void* out, hipStream_t st) {
   if (d % 4 || d > 4 * 64 * MAXV) return hipErrorInvalidValue;
   const dim3 g(nblk(M, 4)), b(256);
+  if (h16) {  // 16-bit residual stream: input and output in the operand dtype
+    if (compute != F5H_C_BF16 && compute != F5H_C_FP16) return hipErrorInvalidValue;
+    auto run = [&](auto tag) {
+      typedef decltype(tag) T;
+      const T* x = (const T*)hv;
+      switch (d) {
+        case 1024: hipLaunchKernelGGL((ln_mod_kernel<T, 4, T>), g, b, 0, st, x, M, d, shift, scale, (T*)out); break;
+        case 768: hipLaunchKernelGGL((ln_mod_kernel<T, 3, T>), g, b, 0, st, x, M, d, shift, scale, (T*)out); break;
+        case 512: hipLaunchKernelGGL((ln_mod_kernel<T, 2, T>), g, b, 0, st, x, M, d, shift, scale, (T*)out); break;
+        default: hipLaunchKernelGGL((ln_mod_kernel<T, 0, T>), g, b, 0, st, x, M, d, shift, scale, (T*)out);
+      }
+    };
+    if (compute == F5H_C_BF16)
+      run(bf16{});
+    else
+      run(f16{});
+    return hipGetLastError();
+  }
+  const float* h = (const float*)hv;
   switch (d) {
     case 1024: F5H_OP_DISPATCH(compute, T, hipLaunchKernelGGL((ln_mod_kernel<T, 4>), g, b, 0, st, h, M, d, shift, scale, (T*)out);); break;
     case 768: F5H_OP_DISPATCH(compute, T, hipLaunchKernelGGL((ln_mod_kernel<T, 3>), g, b, 0, st, h, M, d, shift, scale, (T*)out);); break;

@@ -619,7 +619,15 @@ static int backbone_part(Ctx& c, int s0, int ns, hipStream_t st) {
   const size_t no = (size_t)s0 * c.N;  // first row in the N-row input-embedding buffers
   auto op = [&](void* base, size_t row, size_t width) -> void* { return (char*)base + row * width * es; };
   const uint8_t* keep = c.batch_mask ? b.rowkeep + ro : nullptr;
-  float* bh = b.h + ro * d;
+  // residual stream h: fp32, or the operand dtype on the 16-bit DiT path (as the reference keeps it in
+  // the parameter dtype); UNetT keeps fp32 (its skip connections and time token)
+  static const bool res32 = [] {  // F5H_RES32=1: fp32 residual on the 16-bit path too (A/B)
+    const char* v = getenv("F5H_RES32");
+    return v && *v == '1';
+  }();
+  const bool r16 = bf != 0 && dit && !res32;
+  const size_t hsz = r16 ? es : sizeof(float);
+  void* bh = (char*)b.h + ro * d * hsz;
   float* bh2 = b.h2 ? b.h2 + ro * d : nullptr;
   void* aop = op(b.aop, ro, d);
   void* q = op(b.q, ro, inner);
@@ -655,37 +663,38 @@ static int backbone_part(Ctx& c, int s0, int ns, hipStream_t st) {
     cv.x_f32 = bf ? 0 : 1;
     cv.w = e->conv_w[1];
     cv.bias = e->conv_b[1];
-    cv.mode = 1;
+    cv.mode = r16 ? 2 : 1;
     cv.y = bh;
     cv.y_seq_stride = c.L;
     cv.y_row_off = dit ? 0 : 1;
     cv.resid = b.h0 + no * d;
     KCK(conv_pos(bf, cv, st));
   }
-  if (!dit) KCK(write_time_token(b.temb_cur, ns, c.L, d, bh, st));
+  if (!dit) KCK(write_time_token(b.temb_cur, ns, c.L, d, (float*)bh, st));
 
   const float* ada_k = dit ? b.ada_cur : nullptr;
-  float* h = bh;
-  float* h2 = bh2;
+  const int epi_resid = r16 ? EPI_RESID16 : EPI_RESID;
+  void* h = bh;
+  void* h2 = bh2;
   for (int l = 0; l < a.depth; ++l) {
     Layer& Ly = e->layers[l];
     const float* ad = ada_k ? ada_k + (size_t)l * 6 * d : nullptr;
     if (!dit) {
       if (l < a.depth / 2) {
         // skips are only ever GEMM A operands: keep them in the operand dtype
-        KCK(f32_to_op(bf, h, (int64_t)rows * d, op(b.skips[l], ro, d), st));
+        KCK(f32_to_op(bf, (const float*)h, (int64_t)rows * d, op(b.skips[l], ro, d), st));
       } else {
         // skip_proj(cat(x, skip)) = x.W1^T + skip.W2^T (unett.py:288-297)
-        KCK(f32_to_op(bf, h, (int64_t)rows * d, aop, st));
+        KCK(f32_to_op(bf, (const float*)h, (int64_t)rows * d, aop, st));
         GemmArgs g = gargs(aop, d, Ly.skip1, rows, h2, d);
         KCK(gemm(bf, EPI_STORE, g, st));
         g = gargs(op(b.skips[a.depth - 1 - l], ro, d), d, Ly.skip2, rows, h2, d);
         KCK(gemm(bf, EPI_RESID, g, st));
         std::swap(h, h2);
       }
-      KCK(rms_norm_g(bf, h, rows, d, Ly.g_attn, aop, st));
+      KCK(rms_norm_g(bf, (const float*)h, rows, d, Ly.g_attn, aop, st));
     } else {
-      KCK(ln_modulate(bf, h, rows, d, ad /*shift_msa*/, ad + d /*scale_msa*/, aop, st));
+      KCK(ln_modulate(bf, h, r16, rows, d, ad /*shift_msa*/, ad + d /*scale_msa*/, aop, st));
     }
     {
       GemmArgs g = gargs(aop, d, Ly.qkv, rows, nullptr, 0);
@@ -720,14 +729,14 @@ static int backbone_part(Ctx& c, int s0, int ns, hipStream_t st) {
       g.gate = ad ? ad + 2 * d : nullptr;  // gate_msa
       g.rowkeep = keep;                    // masked_fill of pad rows (modules.py:552-554)
       ProbeScope ps(e, KC_OUT, st, &c.site, &g.probe);
-      KCK(gemm(bf, EPI_RESID, g, st));
+      KCK(gemm(bf, epi_resid, g, st));
     }
     {
       ProbeScope ps(e, KC_NORM, st, &c.site);
       if (dit)
-        KCK(ln_modulate(bf, h, rows, d, ad + 3 * d /*shift_mlp*/, ad + 4 * d /*scale_mlp*/, aop, st));
+        KCK(ln_modulate(bf, h, r16, rows, d, ad + 3 * d /*shift_mlp*/, ad + 4 * d /*scale_mlp*/, aop, st));
       else
-        KCK(rms_norm_g(bf, h, rows, d, Ly.g_ff, aop, st));
+        KCK(rms_norm_g(bf, (const float*)h, rows, d, Ly.g_ff, aop, st));
     }
     {
       GemmArgs g = gargs(aop, d, Ly.ff1, rows, f, a.ff_dim);
@@ -738,14 +747,14 @@ static int backbone_part(Ctx& c, int s0, int ns, hipStream_t st) {
       GemmArgs g = gargs(f, a.ff_dim, Ly.ff2, rows, h, d);
       g.gate = ad ? ad + 5 * d : nullptr;  // gate_mlp
       ProbeScope ps(e, KC_FFN2, st, &c.site, &g.probe);
-      KCK(gemm(bf, EPI_RESID, g, st));
+      KCK(gemm(bf, epi_resid, g, st));
     }
   }
   if (dit) {
     const float* fin = ada_k + (size_t)a.depth * 6 * d;  // AdaLayerNorm_Final: (scale, shift)
-    KCK(ln_modulate(bf, h, rows, d, fin + d, fin, aop, st));
+    KCK(ln_modulate(bf, h, r16, rows, d, fin + d, fin, aop, st));
   } else {
-    KCK(rms_norm_g(bf, h, rows, d, e->norm_out_g, aop, st));
+    KCK(rms_norm_g(bf, (const float*)h, rows, d, e->norm_out_g, aop, st));
   }
   GemmArgs g = gargs(aop, d, e->proj_out, rows, b.p + ro * a.mel_dim, a.mel_dim);
   KCK(gemm(bf, EPI_STORE, g, st));

@@ -69,9 +69,9 @@ hipError_t gemm_launch_f16_a(int epi, const GemmArgs& a, hipStream_t st);
 hipError_t gemm_launch_f16_b(int epi, const GemmArgs& a, hipStream_t st);
 hipError_t gemm_launch_f32(int epi, const GemmArgs& a, hipStream_t st);
 
-// the hot epilogues (QKV, RESID, GELU-tanh, GELU-erf operand) in the *_a units, the rest in *_b
+// the hot epilogues (QKV, RESID, RESID16, GELU-tanh, GELU-erf operand) in the *_a units, the rest in *_b
 static bool hot_epi(int epi) {
-  return epi == EPI_QKV || epi == EPI_RESID || epi == EPI_GELU_TANH || epi == EPI_GELU_ERF_OP;
+  return epi == EPI_QKV || epi == EPI_RESID || epi == EPI_RESID16 || epi == EPI_GELU_TANH || epi == EPI_GELU_ERF_OP;
 }
 
 void gemm_force_config(int cfg) { g_force_cfg = cfg; }

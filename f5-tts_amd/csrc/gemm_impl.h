@@ -106,6 +106,17 @@ F5H_DEV V8 load8(const float* p) {
   float4 a = *reinterpret_cast<const float4*>(p), b = *reinterpret_cast<const float4*>(p + 4);
   return V8{{a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w}};
 }
+F5H_DEV V8 load8(const bf16* p) {
+  const bf16x8 v = *reinterpret_cast<const bf16x8*>(p);
+  return V8{{(float)v[0], (float)v[1], (float)v[2], (float)v[3], (float)v[4], (float)v[5], (float)v[6], (float)v[7]}};
+}
+F5H_DEV V8 load8(const f16* p) {
+  const f16x8 v = *reinterpret_cast<const f16x8*>(p);
+  return V8{{(float)v[0], (float)v[1], (float)v[2], (float)v[3], (float)v[4], (float)v[5], (float)v[6], (float)v[7]}};
+}
+// the residual stream's element type: fp32, or the operand dtype for EPI_RESID16
+template <typename TC, int EPI>
+using ResT = typename std::conditional<EPI == EPI_RESID16, TC, float>::type;
 
 // Epilogue arithmetic with explicit rounding (no FMA contraction), shared by every kernel so that
 // all tile configurations stay bitwise identical whatever the compiler contracts around them.
@@ -164,7 +175,27 @@ F5H_DEV void epi8(const GemmArgs& g, int row, int col, V8 x, const V8* pre = nul
   }
   const int64_t off = (int64_t)row * g.ldc + col;
   const bool vec = full && (g.ldc % 4 == 0);
-  if constexpr (EPI == EPI_GELU_TANH || EPI == EPI_GELU_ERF_OP) {
+  if constexpr (EPI == EPI_RESID16) {
+    // 16-bit residual stream: read, add in fp32 (same rounding as EPI_RESID), store rounded
+    TC* C = reinterpret_cast<TC*>(g.C);
+    const float keep = (g.rowkeep && !g.rowkeep[row]) ? 0.f : 1.f;
+    const bool v16 = full && (g.ldc % 8 == 0);
+    V8 c = v16 ? load8(C + off) : V8{};
+    if (!v16)
+      for (int e = 0; e < 8; ++e) c.v[e] = col + e < g.N ? to_f32(C[off + e]) : 0.f;
+    V8 gt = g.gate ? (full ? load8(g.gate + col) : V8{}) : V8{{1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f}};
+    if (g.gate && !full)
+      for (int e = 0; e < 8; ++e) gt.v[e] = col + e < g.N ? g.gate[col + e] : 0.f;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) x.v[e] = resid_add(c.v[e], gt.v[e], x.v[e], keep);
+    if (v16) {
+      store8<TC>(C + off, x);
+    } else {
+      for (int e = 0; e < 8; ++e)
+        if (col + e < g.N) C[off + e] = from_f32<TC>(x.v[e]);
+    }
+    return;
+  } else if constexpr (EPI == EPI_GELU_TANH || EPI == EPI_GELU_ERF_OP) {
 #pragma unroll
     for (int e = 0; e < 8; ++e)
       x.v[e] = EPI == EPI_GELU_ERF_OP ? gelu_erf(x.v[e])
@@ -322,11 +353,11 @@ __global__ __launch_bounds__(64 * WGM * WGN, 1) void gemm_kernel(GemmArgs g) {
   // oldest VMEM ops, retired by the first stage wait), so the epilogue's read-modify-write does
   // not expose a dependent HBM/MALL round trip. Register budget: small tiles only.
   constexpr int CH_ = WN / 8, TPS = 16 * CH_ / 64;
-  constexpr bool PREF = EPI == EPI_RESID && is16<TC>() && (16 * CH_) % 64 == 0 &&
+  constexpr bool PREF = (EPI == EPI_RESID || EPI == EPI_RESID16) && is16<TC>() && (16 * CH_) % 64 == 0 &&
                         MT * TPS * 8 <= 32;
   V8 pre[PREF ? MT : 1][PREF ? TPS : 1];
   if constexpr (PREF) {
-    const float* Cp = reinterpret_cast<const float*>(g.C);
+    const ResT<TC, EPI>* Cp = reinterpret_cast<const ResT<TC, EPI>*>(g.C);
     const int fr_ = lane & 15, q_ = lane >> 4;
     (void)fr_;
     (void)q_;
@@ -425,7 +456,7 @@ __global__ __launch_bounds__(64 * WGM * WGN, 1) void gemm_kernel(GemmArgs g) {
       const int col = n0 + wn * WN + cc * 8;
       V8 bias8 = g.bias ? load8(g.bias + col) : V8{};
       V8 gate8 = V8{{1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f}};
-      if constexpr (EPI == EPI_RESID)
+      if constexpr (EPI == EPI_RESID || EPI == EPI_RESID16)
         if (g.gate) gate8 = load8(g.gate + col);
       int which = 0, head = 0, dh = 0;
       bool rope_on = false;
@@ -458,11 +489,11 @@ __global__ __launch_bounds__(64 * WGM * WGN, 1) void gemm_kernel(GemmArgs g) {
               const int pos = row - fdiv(row, g.seq_len) * g.seq_len;
               ri[t].d = load8(reinterpret_cast<const float*>(g.rope + (int64_t)pos * 32 + (dh >> 1)));
             }
-          } else if constexpr (EPI == EPI_RESID) {
+          } else if constexpr (EPI == EPI_RESID || EPI == EPI_RESID16) {
             if constexpr (PREF) {
               ri[t].d = V8{};
             } else {
-              ri[t].d = ok ? load8(reinterpret_cast<const float*>(g.C) + (int64_t)row * g.ldc + col) : V8{};
+              ri[t].d = ok ? load8(reinterpret_cast<const ResT<TC, EPI>*>(g.C) + (int64_t)row * g.ldc + col) : V8{};
             }
             if (ok && g.rowkeep && !g.rowkeep[row]) ri[t].keep = 0.f;
           } else {
@@ -520,6 +551,12 @@ __global__ __launch_bounds__(64 * WGM * WGN, 1) void gemm_kernel(GemmArgs g) {
 #pragma unroll
               for (int e = 0; e < 8; ++e) o.v[e] = resid_add(c.v[e], gate8.v[e], x.v[e], ri.keep);
               store8<float>(reinterpret_cast<float*>(g.C) + (int64_t)row * g.ldc + col, o);
+            } else if constexpr (EPI == EPI_RESID16) {
+              V8 o;
+              const V8& c = PREF ? pre[PREF ? i : 0][PREF ? t : 0] : ri.d;
+#pragma unroll
+              for (int e = 0; e < 8; ++e) o.v[e] = resid_add(c.v[e], gate8.v[e], x.v[e], ri.keep);
+              store8<TC>(reinterpret_cast<TC*>(g.C) + (int64_t)row * g.ldc + col, o);
             } else if constexpr (EPI == EPI_GELU_TANH || EPI == EPI_GELU_ERF_OP) {
 #pragma unroll
               for (int e = 0; e < 8; ++e)
@@ -781,8 +818,8 @@ static void launch_pp(const GemmArgs& a, hipStream_t st) {
 template <typename TC, int EPI, int BM, int BN, int WGM, int WGN, int NS, int KB = 128>
 static void launch_cfg(const GemmArgs& a, hipStream_t st) {
   const int tiles = ((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN);
-  constexpr bool HOT = EPI == EPI_QKV || EPI == EPI_RESID || EPI == EPI_GELU_TANH || EPI == EPI_GELU_ERF_OP ||
-                       EPI == EPI_STORE;
+  constexpr bool HOT = EPI == EPI_QKV || EPI == EPI_RESID || EPI == EPI_RESID16 || EPI == EPI_GELU_TANH ||
+                       EPI == EPI_GELU_ERF_OP || EPI == EPI_STORE;
   if constexpr (HOT) {
     if (a.N % BN == 0 && (EPI == EPI_QKV || a.ldc % 8 == 0)) {
       hipLaunchKernelGGL((gemm_kernel<TC, EPI, BM, BN, WGM, WGN, NS, true, KB>), dim3(tiles), dim3(64 * WGM * WGN), 0,
@@ -822,6 +859,7 @@ static hipError_t launch_epi(int epi, const GemmArgs& a, hipStream_t st) {
     case EPI_GELU_TANH: return launch_t<TC, EPI_GELU_TANH>(a, st);
     case EPI_GELU_ERF: return launch_t<TC, EPI_GELU_ERF>(a, st);
     case EPI_RESID: return launch_t<TC, EPI_RESID>(a, st);
+    case EPI_RESID16: return launch_t<TC, EPI_RESID16>(a, st);
     case EPI_RESID_FILL: return launch_t<TC, EPI_RESID_FILL>(a, st);
     case EPI_INPROJ: return launch_t<TC, EPI_INPROJ>(a, st);
     case EPI_QKV: return launch_t<TC, EPI_QKV>(a, st);

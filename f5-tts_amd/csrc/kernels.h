@@ -19,6 +19,7 @@ enum Epi {
   EPI_INPROJ = 6,     // C[m] = acc + add[m]; C[m+dual] = acc + add[m+dual]  (fp32)
   EPI_QKV = 7,        // RoPE + scatter to q/k/v [S,H,L,64]              (operand out)
   EPI_GELU_ERF_OP = 8,  // C = gelu_erf(acc + bias)                      (operand out; Vocos pwconv1)
+  EPI_RESID16 = 9,   // C += gate[n] * (acc + bias) * rowkeep[m]        (operand dtype in/out: 16-bit residual)
 };
 
 // In-kernel launch probe (see probe_enter/probe_exit in common.h). Per launch site a row of
@@ -76,7 +77,8 @@ struct ConvArgs {
   const float* bias;               // [d]
   const uint8_t* rowkeep;          // [S*L] or null: input rows masked, output rows masked
   int S, L, d;
-  // output: mode 0 -> y (operand dtype) = mish(mask(conv)); mode 1 -> y fp32 = mish(mask(conv)) + resid
+  // output: mode 0 -> y (operand dtype) = mish(mask(conv)); mode 1 -> y fp32 = mish(mask(conv)) + resid;
+  // mode 2 (16-bit operands) -> y operand dtype = mish(mask(conv)) + resid (the 16-bit residual stream)
   int mode;
   void* y; int64_t y_seq_stride; int64_t y_row_off;  // in rows
   const float* resid;              // [S, L, d] fp32 (mode 1)
@@ -86,8 +88,9 @@ hipError_t conv_pos(int compute, const ConvArgs& a, hipStream_t st);
 // ---- elementwise / small kernels (elementwise.hip)
 hipError_t time_sinus(const float* t_host, int n, float* out, hipStream_t st);  // host t[n<=512] -> [n,256]
 hipError_t silu_to_op(int compute, const float* x, void* y, int64_t n, hipStream_t st);
-// LayerNorm(no affine, eps) * (1 + scale) + shift -> operand dtype; h: [M, d] fp32
-hipError_t ln_modulate(int compute, const float* h, int M, int d, const float* shift, const float* scale,
+// LayerNorm(no affine, eps) * (1 + scale) + shift -> operand dtype; h: [M, d] fp32, or the operand
+// dtype when h16 (the 16-bit residual stream of the bf16/fp16 DiT path)
+hipError_t ln_modulate(int compute, const void* h, int h16, int M, int d, const float* shift, const float* scale,
                        void* out, hipStream_t st);
 // x_transformers RMSNorm: x / max(||x||, 1e-12) * sqrt(d) * g -> operand dtype
 hipError_t rms_norm_g(int compute, const float* h, int M, int d, const float* g, void* out, hipStream_t st);

@@ -331,7 +331,7 @@ int f5h_vocos_decode(f5h_vocos* v, void* stream, int32_t B, int32_t T, const flo
   // backbone (vocos VocosBackbone.forward): embed -> LayerNorm -> ConvNeXt blocks -> final LayerNorm
   VK(vocos_im2col(bf, mel, B, T, a.input_channels, v->kemb, b.col, st));
   VK(gemm(bf, EPI_STORE, vg(b.col, v->kemb, v->embed, R, b.x0, d), st));
-  VK(ln_modulate(0, b.x0, R, d, v->norm_b, v->norm_sm1, b.x, st));
+  VK(ln_modulate(0, b.x0, 0, R, d, v->norm_b, v->norm_sm1, b.x, st));
   for (const VBlock& blk : v->blocks) {
     VK(dwconv_ln(bf, b.x, B, T, d, blk.dw_w, blk.dw_b, blk.ln_w, blk.ln_b, b.dwln, st));
     VK(gemm(bf, EPI_GELU_ERF_OP, vg(b.dwln, d, blk.pw1, R, b.hid, I), st));
@@ -339,7 +339,7 @@ int f5h_vocos_decode(f5h_vocos* v, void* stream, int32_t B, int32_t T, const flo
     g.gate = blk.gamma;  // x += gamma * pwconv2(.)
     VK(gemm(bf, EPI_RESID, g, st));
   }
-  VK(ln_modulate(0, b.x, R, d, v->fnorm_b, v->fnorm_sm1, b.fln, st));
+  VK(ln_modulate(0, b.x, 0, R, d, v->fnorm_b, v->fnorm_sm1, b.fln, st));
   // head (ISTFTHead.forward), fp32: Linear -> (mag, phase) -> (re, im) -> iDFT frames -> overlap-add
   VK(gemm(0, EPI_STORE, vg(b.fln, d, v->head, R, b.spec, v->kd), st));
   VK(vocos_spec(b.spec, R, v->bins, v->kd, st));
