@@ -44,16 +44,17 @@ def classify(disp):
     return cls
 
 
-def algorithmic(c, S=2, L=1876, d=1024, ff=2048, H=16, es=2):
+def algorithmic(c, S=2, L=1876, d=1024, ff=2048, H=16, es=2, rb=2):
+    """rb: residual stream width (2 on the 16-bit DiT path since EPI_RESID16, 4 with F5H_RES32=1)."""
     rows = S * L
-    gemm = {"qkv": (d, 3 * d, es), "out": (d, d, 8), "ffn1": (d, ff, es), "ffn2": (ff, d, 8)}
+    gemm = {"qkv": (d, 3 * d, es), "out": (d, d, 2 * rb), "ffn1": (d, ff, es), "ffn2": (ff, d, 2 * rb)}
     if c in gemm:
         K, N, out_b = gemm[c]
         return es * (rows * K + N * K) + out_b * rows * N
     if c == "attention":
         return 4 * es * S * H * L * 64  # q, k, v read + o written
     if c in ("norm", "norm1"):
-        return rows * d * (4 + es)
+        return rows * d * (rb + es)
     return None
 
 
