@@ -37,8 +37,9 @@ enum f5h_status {
 };
 
 enum f5h_backbone { F5H_DIT = 0, F5H_UNETT = 1 };
-/* Operand dtype of the GEMM / attention / conv MFMAs. Accumulation, the residual stream, norms,
- * softmax statistics and the ODE state are fp32 in every mode.
+/* Operand dtype of the GEMM / attention / conv MFMAs. Accumulation, norm and softmax statistics and
+ * the ODE state are fp32 in every mode; the residual stream is fp32 except on the DiT path in the
+ * 16-bit modes, where it is kept in the operand dtype as the reference keeps it in the parameter dtype.
  *   F5H_FP32: parity mode (exact-f32 MFMA, VALU attention), the <=1e-3 contract;
  *   F5H_BF16: bf16 operands (the BASELINE configs' dtype);
  *   F5H_FP16: fp16 operands = the reference's default GPU dtype (load_checkpoint casts to fp16 on
