@@ -35,3 +35,14 @@ def test_probe_class_flops():
     assert bench.class_flops("ffn1", arch, S, L) == pytest.approx(15.7e9, rel=3e-3)
     assert bench.class_flops("conv", arch, S, L) == pytest.approx(15.26e9, rel=3e-3)
     assert bench.class_flops("norm", arch, S, L) == 0.0  # HBM-bound: no FLOP roofline
+
+
+def test_norm_bytes_follow_the_residual_width():
+    """The pre-FFN LayerNorm reads the residual rows at the residual stream's width: the operand
+    dtype on the 16-bit DiT path (engine.cpp backbone_part, EPI_RESID16), fp32 on the UNetT path."""
+    S, L = 2, 1876
+    dit, unett = configs.get_arch("F5TTS_v1_Base"), configs.get_arch("E2TTS_Base")
+    assert bench.resid_bytes(dit) == 2 and bench.resid_bytes(unett) == 4
+    assert bench.resid_bytes(dit, esz=4) == 4  # fp32 parity mode
+    assert bench.class_bytes("norm", dit, S, L) == S * L * 1024 * (2 + 2)  # 15.37 MB
+    assert bench.class_bytes("norm", unett, S, L) == S * L * 1024 * (4 + 2)
