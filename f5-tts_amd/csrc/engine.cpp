@@ -706,7 +706,7 @@ static int backbone_part(Ctx& c, int s0, int ns, hipStream_t st) {
   bool fold = false;
   if (b.wf && r16) {
     GemmArgs go = gargs(o, inner, e->layers[0].out, rows, bh, d), gf = gargs(bh, d, e->layers[0].ff1, rows, f, a.ff_dim);
-    fold = gemm_fast_epilogue(bf, go) && gemm_fast_epilogue(bf, gf) && d % 64 == 0 && d <= 2048;
+    fold = gemm_fast_epilogue(bf, go) && gemm_fast_epilogue(bf, gf) && d % 64 == 0;
   }
   float* lnst = fold ? b.lnst + ro * (d / 32) : nullptr;
   void* h = bh;

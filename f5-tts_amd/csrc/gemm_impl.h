@@ -142,28 +142,15 @@ F5H_DEV void ln_row_stats(const GemmArgs& g, int row, float& mu, float& rstd) {
 // lane layout): lane cc sums partials cc, cc+8, ..., then a fixed butterfly; every lane ends with them.
 F5H_DEV float dpp_xor1(float v) { return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0xB1, 0xF, 0xF, false)); }
 F5H_DEV float dpp_xor2(float v) { return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x4E, 0xF, 0xF, false)); }
-// Split in two so the strip loop can prefetch: the loads (partials cc, cc+8, cc+16, cc+24 as
-// (sum, sumsq) pairs into a V8; ln_d <= 2048) and the reduction, done when the strip is consumed.
-F5H_DEV V8 ln_row_load8(const GemmArgs& g, int row, int cc, bool ok) {
-  V8 r{};
+F5H_DEV void ln_row_stats8(const GemmArgs& g, int row, int cc, bool ok, float& mu, float& rstd) {
+  float s = 0.f, q = 0.f;
   if (ok) {
     const float2* p = reinterpret_cast<const float2*>(g.lnst + (int64_t)row * (g.ln_d / 32));
-#pragma unroll
-    for (int j = 0; j < 4; ++j)
-      if (cc + 8 * j < g.ln_d / 64) {
-        const float2 v = p[cc + 8 * j];
-        r.v[2 * j] = v.x;
-        r.v[2 * j + 1] = v.y;
-      }
-  }
-  return r;
-}
-F5H_DEV void ln_row_reduce8(const GemmArgs& g, const V8& r, float& mu, float& rstd) {
-  float s = 0.f, q = 0.f;
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    s = add_nc(s, r.v[2 * j]);
-    q = add_nc(q, r.v[2 * j + 1]);
+    for (int i = cc; i < g.ln_d / 64; i += 8) {
+      const float2 v = p[i];
+      s = add_nc(s, v.x);
+      q = add_nc(q, v.y);
+    }
   }
   s = add_nc(s, dpp_xor1(s));
   q = add_nc(q, dpp_xor1(q));
@@ -561,13 +548,14 @@ __global__ __launch_bounds__(64 * WGM * WGN, 1) void gemm_kernel(GemmArgs g) {
               ri[t].d = load8(reinterpret_cast<const float*>(g.rope + (int64_t)pos * 32 + (dh >> 1)));
             }
           } else if constexpr (EPI == EPI_FOLD_GELU) {
+            float mu, rs;
             if constexpr (CH == 8) {
-              ri[t].d = ln_row_load8(g, row, lane % CH, ok);  // reduced when the strip is consumed
+              ln_row_stats8(g, row, lane % CH, ok, mu, rs);
             } else {
-              float mu = 0.f, rs = 0.f;
+              mu = 0.f, rs = 0.f;
               if (ok) ln_row_stats(g, row, mu, rs);
-              ri[t].d = V8{{mu, rs, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f}};
             }
+            ri[t].d = V8{{mu, rs, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f}};
           } else if constexpr (EPI == EPI_RESID || EPI == EPI_RESID16) {
             if constexpr (PREF) {
               ri[t].d = V8{};
@@ -605,15 +593,6 @@ __global__ __launch_bounds__(64 * WGM * WGN, 1) void gemm_kernel(GemmArgs g) {
           }
           const RowIn& ri = rbuf[i & 1][t];
           V8 o16{};
-          float fmu = 0.f, frs = 0.f;  // EPI_FOLD_GELU row statistics (all lanes: DPP reduction)
-          if constexpr (EPI == EPI_FOLD_GELU) {
-            if constexpr (CH == 8) {
-              ln_row_reduce8(g, ri.d, fmu, frs);
-            } else {
-              fmu = ri.d.v[0];
-              frs = ri.d.v[1];
-            }
-          }
           if constexpr (EPI == EPI_RESID16) {
             const V8& c = PREF ? pre[PREF ? i : 0][PREF ? t : 0] : ri.d;
 #pragma unroll
@@ -670,8 +649,9 @@ __global__ __launch_bounds__(64 * WGM * WGN, 1) void gemm_kernel(GemmArgs g) {
             } else if constexpr (EPI == EPI_RESID16) {
               store8<TC>(reinterpret_cast<TC*>(g.C) + (int64_t)row * g.ldc + col, o16);
             } else if constexpr (EPI == EPI_FOLD_GELU) {
+              const float mu = ri.d.v[0], rs = ri.d.v[1];
 #pragma unroll
-              for (int e = 0; e < 8; ++e) x.v[e] = fold_gelu(x.v[e], fmu, frs, fc8.v[e], fb8.v[e]);
+              for (int e = 0; e < 8; ++e) x.v[e] = fold_gelu(x.v[e], mu, rs, fc8.v[e], fb8.v[e]);
               store8<TC>(reinterpret_cast<TC*>(g.C) + (int64_t)row * g.ldc + col, x);
             } else if constexpr (EPI == EPI_GELU_TANH || EPI == EPI_GELU_ERF_OP) {
 #pragma unroll
