@@ -609,60 +609,4 @@ hipError_t op_to_f32(int compute, const void* x, int64_t n, float* out, hipStrea
   return hipGetLastError();
 }
 
-
-// ---------------------------------------------------------------- LayerNorm fold preparation
-// One wave per (weight row n, step t): Wp[t][n] = W[n] * (1 + scale_t) rounded to the operand dtype,
-// fc[t][n] = sum of the ROUNDED Wp row (so u - mu*fc cancels the row mean exactly in the rounding of
-// Wp), fb[t][n] = shift_t . W[n] + bias[n]; both sums in a fixed order (lane strides, then a butterfly).
-template <typename T>
-__global__ __launch_bounds__(256) void lnfold_prep_kernel(const T* W, const float* bias, int N, int K,
-                                                          const float* table, int64_t trow, int64_t scale_off,
-                                                          int64_t shift_off, T* Wp, int64_t wstride, float* fc,
-                                                          float* fb, int64_t fstride) {
-  const int n = blockIdx.x * 4 + (threadIdx.x >> 6), t = blockIdx.y, lane = threadIdx.x & 63;
-  if (n >= N) return;
-  const float* sc = table + t * trow + scale_off;
-  const float* sh = table + t * trow + shift_off;
-  const T* w = W + (int64_t)n * K;
-  T* wp = Wp + t * wstride + (int64_t)n * K;
-  float s1 = 0.f, s2 = 0.f;
-  for (int k = lane * 8; k < K; k += 512) {
-    typedef typename Op16<T>::v8 v8;
-    const v8 wv = *reinterpret_cast<const v8*>(w + k);
-    v8 o;
-#pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      const float x = to_f32(wv[e]);
-      o[e] = from_f32<T>(x * (1.f + sc[k + e]));
-      s1 += to_f32(o[e]);
-      s2 += sh[k + e] * x;
-    }
-    *reinterpret_cast<v8*>(wp + k) = o;
-  }
-#pragma unroll
-  for (int m = 32; m > 0; m >>= 1) {
-    s1 += __shfl_xor(s1, m);
-    s2 += __shfl_xor(s2, m);
-  }
-  if (lane == 0) {
-    fc[t * fstride + n] = s1;
-    fb[t * fstride + n] = s2 + (bias ? bias[n] : 0.f);
-  }
-}
-hipError_t lnfold_prep(int compute, const void* W, const float* bias, int N, int K, int nt, const float* table,
-                       int64_t trow, int64_t scale_off, int64_t shift_off, void* Wp, int64_t wstride, float* fc,
-                       float* fb, int64_t fstride, hipStream_t st) {
-  if (K % 8 || nt <= 0) return hipErrorInvalidValue;
-  const dim3 g(nblk(N, 4), nt), b(256);
-  if (compute == F5H_C_BF16)
-    hipLaunchKernelGGL(lnfold_prep_kernel<bf16>, g, b, 0, st, (const bf16*)W, bias, N, K, table, trow, scale_off,
-                       shift_off, (bf16*)Wp, wstride, fc, fb, fstride);
-  else if (compute == F5H_C_FP16)
-    hipLaunchKernelGGL(lnfold_prep_kernel<f16>, g, b, 0, st, (const f16*)W, bias, N, K, table, trow, scale_off,
-                       shift_off, (f16*)Wp, wstride, fc, fb, fstride);
-  else
-    return hipErrorInvalidValue;
-  return hipGetLastError();
-}
-
 }  // namespace f5h

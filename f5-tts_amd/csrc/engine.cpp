@@ -415,19 +415,7 @@ struct Bufs {
   float* y;                           // ODE state [B][N][mel] fp32
   float** trajp;                      // device slot: trajectory base pointer (or null)
   std::vector<void*> skips;
-  void* wf;            // LayerNorm fold (F5H_LNFOLD=1): per-step FFN1 weights W(1+scale_mlp) [nfe][depth][N][K]
-  float *ffc, *ffb;    // per-step column vectors rowsum(W'), W.shift_mlp + bias [nfe][depth][N]
-  float* lnst;         // row statistics partials of the residual [rows][d/64][2]
 };
-
-// F5H_LNFOLD=1: fold the DiT block's FFN LayerNorm + AdaLN modulation into the FFN1 GEMM
-static bool lnfold_env() {
-  static const bool on = [] {
-    const char* v = getenv("F5H_LNFOLD");
-    return v && *v == '1';
-  }();
-  return on;
-}
 
 static void layout(const f5h_engine* e, WS& ws, Bufs& b, int B, int N, int nfe, int use_cfg) {
   const f5h_arch& a = e->a;
@@ -474,11 +462,6 @@ static void layout(const f5h_engine* e, WS& ws, Bufs& b, int B, int N, int nfe, 
   b.kstep = ws.take<int>(64);
   b.y = ws.take<float>((size_t)B * N * e->a.mel_dim);
   b.trajp = ws.take<float*>(8);
-  const bool fold = lnfold_env() && e->bf && a.backbone == F5H_DIT;
-  b.wf = fold ? ws.take<char>((size_t)nfe * a.depth * a.ff_dim * d * es) : nullptr;
-  b.ffc = fold ? ws.take<float>((size_t)nfe * a.depth * a.ff_dim) : nullptr;
-  b.ffb = fold ? ws.take<float>((size_t)nfe * a.depth * a.ff_dim) : nullptr;
-  b.lnst = fold ? ws.take<float>(rows * (d / 32)) : nullptr;
   b.skips.clear();
   if (a.backbone == F5H_UNETT)
     for (int i = 0; i < a.depth / 2; ++i) b.skips.push_back(ws.take<char>(rows * d * es));
@@ -571,16 +554,6 @@ static int prologue(Ctx& c, const float* t_host, int nt_vals, const float* cond,
       KCK(silu_to_op(bf, b.temb, b.tin_op, (int64_t)nt_vals * d, st));
       g = gargs(b.tin_op, d, e->ada, nt_vals, b.ada, e->ada.Npad);
       KCK(gemm(bf, EPI_STORE, g, st));
-      if (b.wf) {  // LayerNorm fold: every step's FFN1 weights and column vectors, from the AdaLN table
-        const int ff = a.ff_dim;
-        const int64_t wstride = (int64_t)a.depth * ff * d, fstride = (int64_t)a.depth * ff;
-        for (int l = 0; l < a.depth; ++l) {
-          const Lin& W = e->layers[l].ff1;
-          KCK(lnfold_prep(bf, W.w, W.b, ff, d, nt_vals, b.ada, e->ada.Npad, (int64_t)l * 6 * d + 4 * d,
-                          (int64_t)l * 6 * d + 3 * d, (char*)b.wf + (size_t)l * ff * d * e->esz, wstride,
-                          b.ffc + (size_t)l * ff, b.ffb + (size_t)l * ff, fstride, st));
-        }
-      }
     }
   }
   // ---- text embedding, both branches (cached once per call in the reference, dit.py:294-310)
@@ -701,14 +674,6 @@ static int backbone_part(Ctx& c, int s0, int ns, hipStream_t st) {
 
   const float* ada_k = dit ? b.ada_cur : nullptr;
   const int epi_resid = r16 ? EPI_RESID16 : EPI_RESID;
-  // LayerNorm fold: the out-projection's epilogue writes the residual rows' statistics partials and
-  // FFN1 applies (acc - mu rowsum(W')) rstd + W.shift + b; needs the fast epilogue on both GEMMs
-  bool fold = false;
-  if (b.wf && r16) {
-    GemmArgs go = gargs(o, inner, e->layers[0].out, rows, bh, d), gf = gargs(bh, d, e->layers[0].ff1, rows, f, a.ff_dim);
-    fold = gemm_fast_epilogue(bf, go) && gemm_fast_epilogue(bf, gf) && d % 64 == 0;
-  }
-  float* lnst = fold ? b.lnst + ro * (d / 32) : nullptr;
   void* h = bh;
   void* h2 = bh2;
   for (int l = 0; l < a.depth; ++l) {
@@ -763,33 +728,17 @@ static int backbone_part(Ctx& c, int s0, int ns, hipStream_t st) {
       GemmArgs g = gargs(o, inner, Ly.out, rows, h, d);
       g.gate = ad ? ad + 2 * d : nullptr;  // gate_msa
       g.rowkeep = keep;                    // masked_fill of pad rows (modules.py:552-554)
-      g.lnst = lnst;
-      g.ln_d = d;
       ProbeScope ps(e, KC_OUT, st, &c.site, &g.probe);
       KCK(gemm(bf, epi_resid, g, st));
     }
-    if (fold) {
-      const int ff = a.ff_dim;
-      GemmArgs g = gargs(h, d, Ly.ff1, rows, f, ff);
-      g.W = (char*)b.wf + (size_t)l * ff * d * es;
-      g.bias = nullptr;
-      g.wstep = b.kstep;
-      g.wstride = (int64_t)a.depth * ff * d;
-      g.fc = b.ffc + (size_t)l * ff;
-      g.fb = b.ffb + (size_t)l * ff;
-      g.fstride = (int64_t)a.depth * ff;
-      g.lnst = lnst;
-      g.ln_d = d;
-      ProbeScope ps(e, KC_FFN1, st, &c.site, &g.probe);
-      KCK(gemm(bf, EPI_FOLD_GELU, g, st));
-    } else {
-      {
-        ProbeScope ps(e, KC_NORM, st, &c.site);
-        if (dit)
-          KCK(ln_modulate(bf, h, r16, rows, d, ad + 3 * d /*shift_mlp*/, ad + 4 * d /*scale_mlp*/, aop, st));
-        else
-          KCK(rms_norm_g(bf, (const float*)h, rows, d, Ly.g_ff, aop, st));
-      }
+    {
+      ProbeScope ps(e, KC_NORM, st, &c.site);
+      if (dit)
+        KCK(ln_modulate(bf, h, r16, rows, d, ad + 3 * d /*shift_mlp*/, ad + 4 * d /*scale_mlp*/, aop, st));
+      else
+        KCK(rms_norm_g(bf, (const float*)h, rows, d, Ly.g_ff, aop, st));
+    }
+    {
       GemmArgs g = gargs(aop, d, Ly.ff1, rows, f, a.ff_dim);
       ProbeScope ps(e, KC_FFN1, st, &c.site, &g.probe);
       KCK(gemm(bf, EPI_GELU_TANH, g, st));

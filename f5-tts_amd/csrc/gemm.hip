@@ -71,17 +71,10 @@ hipError_t gemm_launch_f32(int epi, const GemmArgs& a, hipStream_t st);
 
 // the hot epilogues (QKV, RESID, RESID16, GELU-tanh, GELU-erf operand) in the *_a units, the rest in *_b
 static bool hot_epi(int epi) {
-  return epi == EPI_QKV || epi == EPI_RESID || epi == EPI_RESID16 || epi == EPI_FOLD_GELU || epi == EPI_GELU_TANH ||
-         epi == EPI_GELU_ERF_OP;
+  return epi == EPI_QKV || epi == EPI_RESID || epi == EPI_RESID16 || epi == EPI_GELU_TANH || epi == EPI_GELU_ERF_OP;
 }
 
 void gemm_force_config(int cfg) { g_force_cfg = cfg; }
-
-bool gemm_fast_epilogue(int compute, const GemmArgs& a) {
-  if (compute != F5H_C_BF16 && compute != F5H_C_FP16) return false;
-  const int cfg = gemm_select_cfg(a);
-  return (cfg == 0 || cfg == 1 || cfg == 5) && a.N % 128 == 0 && a.ldc % 8 == 0;
-}
 
 hipError_t gemm(int compute, int epi, const GemmArgs& a, hipStream_t st) {
   const int bke = compute ? 64 : 32;

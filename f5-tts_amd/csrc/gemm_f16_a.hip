@@ -7,7 +7,6 @@ hipError_t gemm_launch_f16_a(int epi, const GemmArgs& a, hipStream_t st) {
     case EPI_QKV: return launch_t<f16, EPI_QKV>(a, st);
     case EPI_RESID: return launch_t<f16, EPI_RESID>(a, st);
     case EPI_RESID16: return launch_t<f16, EPI_RESID16>(a, st);
-    case EPI_FOLD_GELU: return launch_t<f16, EPI_FOLD_GELU>(a, st);
     case EPI_GELU_TANH: return launch_t<f16, EPI_GELU_TANH>(a, st);
     case EPI_GELU_ERF_OP: return launch_t<f16, EPI_GELU_ERF_OP>(a, st);
   }

@@ -124,50 +124,6 @@ F5H_DEV float rope_re(float a, float b, float c, float s) { return sub_nc(mul_nc
 F5H_DEV float rope_im(float a, float b, float c, float s) { return add_nc(mul_nc(b, c), mul_nc(a, s)); }
 F5H_DEV float resid_add(float c, float gate, float x, float keep) { return add_nc(c, mul_nc(gate, mul_nc(x, keep))); }
 
-// LayerNorm statistics of row `row` from its ln_d/64 partial (sum, sum of squares) pairs, summed in
-// a fixed order (EPI_FOLD_GELU; the partials are EPI_RESID16's, of the stored 16-bit residual)
-F5H_DEV void ln_row_stats(const GemmArgs& g, int row, float& mu, float& rstd) {
-  const float* p = g.lnst + (int64_t)row * (g.ln_d / 32);
-  float s = 0.f, q = 0.f;
-  for (int i = 0; i < g.ln_d / 64; ++i) {
-    s = add_nc(s, p[2 * i]);
-    q = add_nc(q, p[2 * i + 1]);
-  }
-  const float inv = 1.f / (float)g.ln_d;
-  mu = mul_nc(s, inv);
-  const float var = sub_nc(mul_nc(q, inv), mul_nc(mu, mu));
-  rstd = rsqrtf(add_nc(fmaxf(var, 0.f), 1e-6f));
-}
-// The same statistics, read by the 8 lanes cc = 0..7 that share output row `row` (the fast epilogue's
-// lane layout): lane cc sums partials cc, cc+8, ..., then a fixed butterfly; every lane ends with them.
-F5H_DEV float dpp_xor1(float v) { return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0xB1, 0xF, 0xF, false)); }
-F5H_DEV float dpp_xor2(float v) { return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x4E, 0xF, 0xF, false)); }
-F5H_DEV void ln_row_stats8(const GemmArgs& g, int row, int cc, bool ok, float& mu, float& rstd) {
-  float s = 0.f, q = 0.f;
-  if (ok) {
-    const float2* p = reinterpret_cast<const float2*>(g.lnst + (int64_t)row * (g.ln_d / 32));
-    for (int i = cc; i < g.ln_d / 64; i += 8) {
-      const float2 v = p[i];
-      s = add_nc(s, v.x);
-      q = add_nc(q, v.y);
-    }
-  }
-  s = add_nc(s, dpp_xor1(s));
-  q = add_nc(q, dpp_xor1(q));
-  s = add_nc(s, dpp_xor2(s));
-  q = add_nc(q, dpp_xor2(q));
-  s = add_nc(s, __shfl_xor(s, 4));
-  q = add_nc(q, __shfl_xor(q, 4));
-  const float inv = 1.f / (float)g.ln_d;
-  mu = mul_nc(s, inv);
-  const float var = sub_nc(mul_nc(q, inv), mul_nc(mu, mu));
-  rstd = rsqrtf(add_nc(fmaxf(var, 0.f), 1e-6f));
-}
-// (acc - mu fc) rstd + fb, then GELU-tanh: the folded AdaLN LayerNorm of FFN1 (explicit rounding)
-F5H_DEV float fold_gelu(float acc, float mu, float rstd, float fc, float fb) {
-  return gelu_tanh_fast(add_nc(mul_nc(sub_nc(acc, mul_nc(mu, fc)), rstd), fb));
-}
-
 // n / d for 0 <= n < 2^24, d > 0: float quotient + one-step correction (no integer division loop)
 F5H_DEV int fdiv(int n, int d) {
   int q = (int)((float)n * __builtin_amdgcn_rcpf((float)d));
@@ -219,15 +175,7 @@ F5H_DEV void epi8(const GemmArgs& g, int row, int col, V8 x, const V8* pre = nul
   }
   const int64_t off = (int64_t)row * g.ldc + col;
   const bool vec = full && (g.ldc % 4 == 0);
-  if constexpr (EPI == EPI_FOLD_GELU) {
-    TC* C = reinterpret_cast<TC*>(g.C);
-    float mu, rs;
-    ln_row_stats(g, row, mu, rs);
-    const int64_t fo = g.wstep ? (int64_t)(*g.wstep) * g.fstride : 0;
-    for (int e = 0; e < 8; ++e)
-      if (col + e < g.N) C[off + e] = from_f32<TC>(fold_gelu(x.v[e], mu, rs, g.fc[fo + col + e], g.fb[fo + col + e]));
-    return;
-  } else if constexpr (EPI == EPI_RESID16) {
+  if constexpr (EPI == EPI_RESID16) {
     // 16-bit residual stream: read, add in fp32 (same rounding as EPI_RESID), store rounded
     TC* C = reinterpret_cast<TC*>(g.C);
     const float keep = (g.rowkeep && !g.rowkeep[row]) ? 0.f : 1.f;
@@ -348,7 +296,7 @@ __global__ __launch_bounds__(64 * WGM * WGN, 1) void gemm_kernel(GemmArgs g) {
   const int bid = (xcd < xr ? xcd * (xq + 1) : xr * (xq + 1) + (xcd - xr) * xq) + (b >> 3);
   const int m0 = (bid / ntn) * BM, n0 = (bid % ntn) * BN;
   const TC* A = reinterpret_cast<const TC*>(g.A);
-  const TC* W = reinterpret_cast<const TC*>(g.W) + (g.wstep ? (int64_t)(*g.wstep) * g.wstride : 0);
+  const TC* W = reinterpret_cast<const TC*>(g.W);
 
   // per-lane DMA source offsets (elements), fixed across K-steps. The swizzle goes on the
   // SOURCE chunk so that (wave-uniform LDS base + lane*16) lands on the swz128 image.
@@ -507,12 +455,6 @@ __global__ __launch_bounds__(64 * WGM * WGN, 1) void gemm_kernel(GemmArgs g) {
       const int cc = lane % CH;
       const int col = n0 + wn * WN + cc * 8;
       V8 bias8 = g.bias ? load8(g.bias + col) : V8{};
-      V8 fc8{}, fb8{};  // EPI_FOLD_GELU: this step's folded-LayerNorm column vectors
-      if constexpr (EPI == EPI_FOLD_GELU) {
-        const int64_t fo = g.wstep ? (int64_t)(*g.wstep) * g.fstride : 0;
-        fc8 = load8(g.fc + fo + col);
-        fb8 = load8(g.fb + fo + col);
-      }
       V8 gate8 = V8{{1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f}};
       if constexpr (EPI == EPI_RESID || EPI == EPI_RESID16)
         if (g.gate) gate8 = load8(g.gate + col);
@@ -547,15 +489,6 @@ __global__ __launch_bounds__(64 * WGM * WGN, 1) void gemm_kernel(GemmArgs g) {
               const int pos = row - fdiv(row, g.seq_len) * g.seq_len;
               ri[t].d = load8(reinterpret_cast<const float*>(g.rope + (int64_t)pos * 32 + (dh >> 1)));
             }
-          } else if constexpr (EPI == EPI_FOLD_GELU) {
-            float mu, rs;
-            if constexpr (CH == 8) {
-              ln_row_stats8(g, row, lane % CH, ok, mu, rs);
-            } else {
-              mu = 0.f, rs = 0.f;
-              if (ok) ln_row_stats(g, row, mu, rs);
-            }
-            ri[t].d = V8{{mu, rs, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f}};
           } else if constexpr (EPI == EPI_RESID || EPI == EPI_RESID16) {
             if constexpr (PREF) {
               ri[t].d = V8{};
@@ -592,34 +525,6 @@ __global__ __launch_bounds__(64 * WGM * WGN, 1) void gemm_kernel(GemmArgs g) {
             for (int e = 0; e < 8; ++e) x.v[e] = add_nc(x.v[e], bias8.v[e]);
           }
           const RowIn& ri = rbuf[i & 1][t];
-          V8 o16{};
-          if constexpr (EPI == EPI_RESID16) {
-            const V8& c = PREF ? pre[PREF ? i : 0][PREF ? t : 0] : ri.d;
-#pragma unroll
-            for (int e = 0; e < 8; ++e) o16.v[e] = resid_add(c.v[e], gate8.v[e], x.v[e], ri.keep);
-            if (WN == 64 && g.lnst) {
-              // LayerNorm partials of the stored (rounded) row chunk: 8 lanes hold one row's 64 columns
-              float s = 0.f, q = 0.f;
-#pragma unroll
-              for (int e = 0; e < 8; ++e) {
-                const float r = to_f32(from_f32<TC>(o16.v[e]));
-                s = add_nc(s, r);
-                q = add_nc(q, mul_nc(r, r));
-              }
-              // lanes 8j..8j+7 hold one row: quad butterflies, then lane 8j adds lane 8j+4 (row_ror:12 reads lane i+4 of the 16-lane row)
-              s = add_nc(s, dpp_xor1(s));
-              q = add_nc(q, dpp_xor1(q));
-              s = add_nc(s, dpp_xor2(s));
-              q = add_nc(q, dpp_xor2(q));
-              s = add_nc(s, __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, s), 0x12C, 0xF, 0xF, false)));
-              q = add_nc(q, __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, q), 0x12C, 0xF, 0xF, false)));
-              if (cc == 0 && row < g.M) {
-                float* pp = g.lnst + (int64_t)row * (g.ln_d / 32) + ((n0 + wn * WN) / 64) * 2;
-                pp[0] = s;
-                pp[1] = q;
-              }
-            }
-          }
           if (row < g.M) {
             if constexpr (EPI == EPI_QKV) {
               if (rope_on) {
@@ -647,12 +552,11 @@ __global__ __launch_bounds__(64 * WGM * WGN, 1) void gemm_kernel(GemmArgs g) {
               for (int e = 0; e < 8; ++e) o.v[e] = resid_add(c.v[e], gate8.v[e], x.v[e], ri.keep);
               store8<float>(reinterpret_cast<float*>(g.C) + (int64_t)row * g.ldc + col, o);
             } else if constexpr (EPI == EPI_RESID16) {
-              store8<TC>(reinterpret_cast<TC*>(g.C) + (int64_t)row * g.ldc + col, o16);
-            } else if constexpr (EPI == EPI_FOLD_GELU) {
-              const float mu = ri.d.v[0], rs = ri.d.v[1];
+              V8 o;
+              const V8& c = PREF ? pre[PREF ? i : 0][PREF ? t : 0] : ri.d;
 #pragma unroll
-              for (int e = 0; e < 8; ++e) x.v[e] = fold_gelu(x.v[e], mu, rs, fc8.v[e], fb8.v[e]);
-              store8<TC>(reinterpret_cast<TC*>(g.C) + (int64_t)row * g.ldc + col, x);
+              for (int e = 0; e < 8; ++e) o.v[e] = resid_add(c.v[e], gate8.v[e], x.v[e], ri.keep);
+              store8<TC>(reinterpret_cast<TC*>(g.C) + (int64_t)row * g.ldc + col, o);
             } else if constexpr (EPI == EPI_GELU_TANH || EPI == EPI_GELU_ERF_OP) {
 #pragma unroll
               for (int e = 0; e < 8; ++e)
@@ -754,7 +658,7 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(GemmArgs g) {
   const int bid = (xcd < xr ? xcd * (xq + 1) : xr * (xq + 1) + (xcd - xr) * xq) + (b >> 3);
   const int m0 = (bid / ntn) * BM, n0 = (bid % ntn) * BN;
   const TC* A = reinterpret_cast<const TC*>(g.A);
-  const TC* W = reinterpret_cast<const TC*>(g.W) + (g.wstep ? (int64_t)(*g.wstep) * g.wstride : 0);
+  const TC* W = reinterpret_cast<const TC*>(g.W);
 
   // ---- DMA: group 0 stages the A rows, group 1 the W rows. Instruction i of wave w4 covers
   // rows (i*4 + w4)*16 .. +15 of its operand; lane -> (row = lane>>2, physical chunk lane&3).
@@ -914,7 +818,7 @@ static void launch_pp(const GemmArgs& a, hipStream_t st) {
 template <typename TC, int EPI, int BM, int BN, int WGM, int WGN, int NS, int KB = 128>
 static void launch_cfg(const GemmArgs& a, hipStream_t st) {
   const int tiles = ((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN);
-  constexpr bool HOT = EPI == EPI_QKV || EPI == EPI_RESID || EPI == EPI_RESID16 || EPI == EPI_FOLD_GELU || EPI == EPI_GELU_TANH ||
+  constexpr bool HOT = EPI == EPI_QKV || EPI == EPI_RESID || EPI == EPI_RESID16 || EPI == EPI_GELU_TANH ||
                        EPI == EPI_GELU_ERF_OP || EPI == EPI_STORE;
   if constexpr (HOT) {
     if (a.N % BN == 0 && (EPI == EPI_QKV || a.ldc % 8 == 0)) {
@@ -956,7 +860,6 @@ static hipError_t launch_epi(int epi, const GemmArgs& a, hipStream_t st) {
     case EPI_GELU_ERF: return launch_t<TC, EPI_GELU_ERF>(a, st);
     case EPI_RESID: return launch_t<TC, EPI_RESID>(a, st);
     case EPI_RESID16: return launch_t<TC, EPI_RESID16>(a, st);
-    case EPI_FOLD_GELU: return launch_t<TC, EPI_FOLD_GELU>(a, st);
     case EPI_RESID_FILL: return launch_t<TC, EPI_RESID_FILL>(a, st);
     case EPI_INPROJ: return launch_t<TC, EPI_INPROJ>(a, st);
     case EPI_QKV: return launch_t<TC, EPI_QKV>(a, st);

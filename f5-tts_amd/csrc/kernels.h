@@ -20,7 +20,6 @@ enum Epi {
   EPI_QKV = 7,        // RoPE + scatter to q/k/v [S,H,L,64]              (operand out)
   EPI_GELU_ERF_OP = 8,  // C = gelu_erf(acc + bias)                      (operand out; Vocos pwconv1)
   EPI_RESID16 = 9,   // C += gate[n] * (acc + bias) * rowkeep[m]        (operand dtype in/out: 16-bit residual)
-  EPI_FOLD_GELU = 10, // C = gelu_tanh((acc - mu[m] fc[n]) rstd[m] + fb[n])  (operand out: AdaLN LayerNorm folded in)
 };
 
 // In-kernel launch probe (see probe_enter/probe_exit in common.h). Per launch site a row of
@@ -52,13 +51,6 @@ struct GemmArgs {
   int heads, rope_heads;
   void* q; void* k; void* v;
   float q_scale;                   // EPI_QKV: q is stored pre-multiplied by this (0 -> 1)
-  // LayerNorm fold: per-step weights W += (*wstep) * wstride (elements); per-step
-  // column vectors fc/fb += (*wstep) * fstride; row statistics partials lnst [M][ln_d/64][2] (sum, sum
-  // of squares of the stored 16-bit residual over 64 columns), written by EPI_RESID16 when non-null on
-  // its fast epilogue, read by EPI_FOLD_GELU
-  const int* wstep; int64_t wstride;
-  const float* fc; const float* fb; int64_t fstride;
-  float* lnst; int ln_d;
   DevProbe probe;                  // in-kernel launch timing (null slots: off)
 };
 
@@ -66,15 +58,6 @@ struct GemmArgs {
 hipError_t gemm(int compute, int epi, const GemmArgs& a, hipStream_t st);
 // pin the 16-bit GEMM tile configuration (0, 1, 5, 11; -1 = automatic choice); tuning and test hook
 void gemm_force_config(int cfg);
-// true when a hot epilogue of this shape runs on the whole-column fast path (16-bit operands, tile
-// configurations 0/1/5): the only path on which EPI_RESID16 writes LayerNorm partials
-bool gemm_fast_epilogue(int compute, const GemmArgs& a);
-// LayerNorm fold preparation for one layer's consuming linear W [Npad][K], steps
-// t < nt: Wp[t] = W * (1 + scale_t) rounded to the operand dtype, fc[t][n] = sum_k Wp[t][n][k],
-// fb[t][n] = sum_k shift_t[k] W[n][k] + bias[n]; scale_t / shift_t = table + t * trow + {scale_off, shift_off}
-hipError_t lnfold_prep(int compute, const void* W, const float* bias, int N, int K, int nt, const float* table,
-                       int64_t trow, int64_t scale_off, int64_t shift_off, void* Wp, int64_t wstride, float* fc,
-                       float* fb, int64_t fstride, hipStream_t st);
 
 // attention: Q,K,V [S,H,L,64] operand dtype; O [S,L,H*64] operand dtype.
 struct AttnArgs {
