@@ -45,6 +45,23 @@ hipError_t time_sinus(const float* t_host, int n, float* out, hipStream_t st) {
   return hipGetLastError();
 }
 
+// The same from the device copy of the grid (the prologue graph: no host values baked in)
+__global__ void time_sinus_dev_kernel(const float* tg, int n, float* out) {
+  int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n * 128) return;
+  int r = i / 128, j = i % 128;
+  const float k = logf(10000.f) / 127.f;
+  float f = expf((float)j * -k);
+  float e = (1000.f * tg[r]) * f;
+  out[r * 256 + j] = sinf(e);
+  out[r * 256 + 128 + j] = cosf(e);
+}
+hipError_t time_sinus_dev(const float* tg, int n, float* out, hipStream_t st) {
+  if (n <= 0 || n > 512) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(time_sinus_dev_kernel, dim3(nblk(n * 128, 256)), dim3(256), 0, st, tg, n, out);
+  return hipGetLastError();
+}
+
 // The ODE grid t[0..n-1] into device memory (kernel-argument upload, capturable).
 __global__ void grid_upload_kernel(TVals tv, int n, float* out) {
   int i = blockIdx.x * blockDim.x + threadIdx.x;

@@ -19,6 +19,7 @@
 #include <algorithm>
 #include <atomic>
 #include <memory>
+#include <functional>
 #include <mutex>
 #include <string>
 #include <unordered_map>
@@ -129,11 +130,12 @@ static std::atomic<uint64_t> g_kernel_epoch{0};
 
 struct GraphKey {
   const void* ws;
-  int B, N, nfe, use_cfg, batch_mask, probe, split;
+  int kind;  // 0: one NFE step, 1: the call prologue (inputs staged into the workspace)
+  int B, N, nt, nfe, use_cfg, batch_mask, probe, split;
   uint64_t kernel_epoch;  // bumped whenever a forced GEMM config changes
   uint32_t cfg_bits;
   bool operator==(const GraphKey& o) const {
-    return ws == o.ws && B == o.B && N == o.N && nfe == o.nfe && kernel_epoch == o.kernel_epoch &&
+    return ws == o.ws && kind == o.kind && B == o.B && N == o.N && nt == o.nt && nfe == o.nfe && kernel_epoch == o.kernel_epoch &&
            use_cfg == o.use_cfg && batch_mask == o.batch_mask && probe == o.probe && cfg_bits == o.cfg_bits &&
            split == o.split;
   }
@@ -415,6 +417,12 @@ struct Bufs {
   float* y;                           // ODE state [B][N][mel] fp32
   float** trajp;                      // device slot: trajectory base pointer (or null)
   std::vector<void*> skips;
+  // the call's inputs staged into the workspace (prologue graph): cond [B][N][mel] fp32,
+  // cond_mask [B][N], text [B][<= N] (int64), duration [B]
+  float* in_cond;
+  uint8_t* in_mask;
+  int64_t* in_text;
+  int32_t* in_dur;
 };
 
 static void layout(const f5h_engine* e, WS& ws, Bufs& b, int B, int N, int nfe, int use_cfg) {
@@ -462,6 +470,10 @@ static void layout(const f5h_engine* e, WS& ws, Bufs& b, int B, int N, int nfe, 
   b.kstep = ws.take<int>(64);
   b.y = ws.take<float>((size_t)B * N * e->a.mel_dim);
   b.trajp = ws.take<float*>(8);
+  b.in_cond = ws.take<float>((size_t)B * N * a.mel_dim);
+  b.in_mask = ws.take<uint8_t>((size_t)B * N);
+  b.in_text = ws.take<int64_t>((size_t)B * N);
+  b.in_dur = ws.take<int32_t>((size_t)B);
   b.skips.clear();
   if (a.backbone == F5H_UNETT)
     for (int i = 0; i < a.depth / 2; ++i) b.skips.push_back(ws.take<char>(rows * d * es));
@@ -543,7 +555,10 @@ static int prologue(Ctx& c, const float* t_host, int nt_vals, const float* cond,
   }
   // ---- time embedding for every grid point used, then the AdaLN table
   {
-    KCK(time_sinus(t_host, nt_vals, b.tsin, st));
+    if (t_host)
+      KCK(time_sinus(t_host, nt_vals, b.tsin, st));
+    else
+      KCK(time_sinus_dev(b.tgrid, nt_vals, b.tsin, st));  // prologue graph: grid uploaded beforehand
     KCK(f32_to_op(bf, b.tsin, (int64_t)nt_vals * 256, b.tin_op, st));
     GemmArgs g = gargs(b.tin_op, 256, e->t1, nt_vals, b.th, d);
     KCK(gemm(bf, EPI_SILU, g, st));
@@ -870,6 +885,38 @@ static int check_ws(f5h_engine* e, int B, int N, int nfe, int use_cfg, void* w, 
 }
 
 static int run_steps(Ctx& c, const f5h_sample_args* a, const void* ws);
+static int graph_get(Ctx& c, const GraphKey& key, bool split, const std::function<int(Ctx&)>& body,
+                     std::shared_ptr<GraphEntry>& hold, int64_t replays);
+
+// The prologue as one captured graph per (workspace, shape): its ~56 launches otherwise cost more
+// host time than device time (profiles/r02_call_gaps_c2.txt). The inputs it reads are staged into
+// fixed workspace slots first, the grid is read from the device copy. F5H_PROLOGUE_GRAPH=0: eager.
+static int prologue_graph(Ctx& c, const f5h_sample_args* a, const void* ws) {
+  f5h_engine* e = c.e;
+  const size_t bn = (size_t)c.B * c.N;
+  HIPCK(hipMemcpyAsync(c.b.in_cond, a->cond, bn * e->a.mel_dim * sizeof(float), hipMemcpyDeviceToDevice, c.st));
+  HIPCK(hipMemcpyAsync(c.b.in_mask, a->cond_mask, bn, hipMemcpyDeviceToDevice, c.st));
+  if (c.nt > 0)
+    HIPCK(hipMemcpyAsync(c.b.in_text, a->text, (size_t)c.B * c.nt * sizeof(int64_t), hipMemcpyDeviceToDevice, c.st));
+  HIPCK(hipMemcpyAsync(c.b.in_dur, a->duration, (size_t)c.B * sizeof(int32_t), hipMemcpyDeviceToDevice, c.st));
+  GraphKey key{};
+  key.ws = ws;
+  key.kind = 1;
+  key.B = c.B;
+  key.N = c.N;
+  key.nt = c.nt;
+  key.nfe = c.nfe;
+  key.use_cfg = c.use_cfg;
+  key.batch_mask = c.batch_mask;
+  key.kernel_epoch = g_kernel_epoch.load();
+  const Bufs& b = c.b;
+  std::shared_ptr<GraphEntry> hold;
+  RC(graph_get(c, key, false,
+               [&](Ctx& cc) { return prologue(cc, nullptr, cc.nfe, b.in_cond, b.in_mask, b.in_text, b.in_dur); },
+               hold, 1));
+  HIPCK(hipGraphLaunch(hold->exec, c.st));
+  return 0;
+}
 
 int f5h_sample(f5h_engine* e, void* stream, const f5h_sample_args* a, void* workspace, size_t workspace_bytes) {
   if (!e || !a) return fail(F5H_EINVAL, "null engine/args");
@@ -891,14 +938,21 @@ int f5h_sample(f5h_engine* e, void* stream, const f5h_sample_args* a, void* work
   c.L = e->a.backbone == F5H_DIT ? c.N : c.N + 1;
   c.batch_mask = a->use_batch_mask ? 1 : 0;
   RC(check_ws(e, c.B, c.N, c.nfe, c.use_cfg, workspace, workspace_bytes, c));
+  static const bool pro_graph = [] {
+    const char* v = getenv("F5H_PROLOGUE_GRAPH");
+    return !(v && *v == '0');
+  }();
+  HIPCK(grid_upload(a->t_grid, c.nfe + 1, c.b.tgrid, c.st));
   // the ODE evaluates fn at t_0 .. t_{nfe-1}
-  RC(prologue(c, a->t_grid, c.nfe, a->cond, a->cond_mask, a->text, a->duration));
+  if (pro_graph && e->graph_mode && c.nt <= c.N)
+    RC(prologue_graph(c, a, workspace));
+  else
+    RC(prologue(c, a->t_grid, c.nfe, a->cond, a->cond_mask, a->text, a->duration));
   const size_t ysz = (size_t)c.B * c.N * e->a.mel_dim;
   HIPCK(hipMemcpyAsync(c.b.y, a->y0, ysz * sizeof(float), hipMemcpyDeviceToDevice, c.st));
   if (a->trajectory)
     HIPCK(hipMemcpyAsync(a->trajectory, a->y0, ysz * sizeof(float), hipMemcpyDeviceToDevice, c.st));
   HIPCK(pack_y(e->bf, c.b.y, c.B * c.N, e->a.mel_dim, c.b.ypad, c.st));
-  HIPCK(grid_upload(a->t_grid, c.nfe + 1, c.b.tgrid, c.st));
   HIPCK(ptr_upload(a->trajectory, c.b.trajp, c.st));
   HIPCK(hipMemsetAsync(c.b.kstep, 0, sizeof(int), c.st));
   RC(run_steps(c, a, workspace));
@@ -958,52 +1012,58 @@ static int run_steps(Ctx& c, const f5h_sample_args* a, const void* ws) {
   key.kernel_epoch = g_kernel_epoch.load();
   std::memcpy(&key.cfg_bits, &a->cfg_strength, 4);
   std::shared_ptr<GraphEntry> hold;  // keeps the replayed graph alive through the launch loop
-  {
-    std::lock_guard<std::mutex> g(e->gm);
-    for (const auto& x : e->graphs)
-      if (x->key == key) hold = x;
-    if (!hold) {
-      if (!e->cap) HIPCK(hipStreamCreateWithFlags(&e->cap, hipStreamNonBlocking));
-      if (split && !e->cap2) {
-        HIPCK(hipStreamCreateWithFlags(&e->cap2, hipStreamNonBlocking));
-        HIPCK(hipEventCreateWithFlags(&e->ev_fork, hipEventDisableTiming));
-        HIPCK(hipEventCreateWithFlags(&e->ev_join, hipEventDisableTiming));
-      }
-      auto ne = std::make_shared<GraphEntry>();
-      ne->key = key;
-      Ctx cc = c;
-      cc.st = e->cap;
-      cc.st2 = split ? e->cap2 : nullptr;
-      hipError_t be = hipStreamBeginCapture(e->cap, hipStreamCaptureModeThreadLocal);
-      if (be != hipSuccess) return fail(F5H_EHIP, std::string("hipStreamBeginCapture: ") + hipGetErrorString(be));
-      const int rc = enqueue_step(cc, a);
-      hipGraph_t graph = nullptr;
-      const hipError_t ce = hipStreamEndCapture(e->cap, &graph);
-      if (rc || ce != hipSuccess) {
-        if (graph) (void)hipGraphDestroy(graph);
-        if (rc) return rc;
-        return fail(F5H_EHIP, std::string("hipStreamEndCapture: ") + hipGetErrorString(ce));
-      }
-      const hipError_t ie = hipGraphInstantiate(&ne->exec, graph, nullptr, nullptr, 0);
-      (void)hipGraphDestroy(graph);
-      if (ie != hipSuccess) {
-        ne->exec = nullptr;
-        return fail(F5H_EHIP, std::string("hipGraphInstantiate: ") + hipGetErrorString(ie));
-      }
-      if (e->graphs.size() >= 8) {  // evict the least recently used step graph
-        size_t lru = 0;
-        for (size_t i = 1; i < e->graphs.size(); ++i)
-          if (e->graphs[i]->stamp < e->graphs[lru]->stamp) lru = i;
-        e->graphs.erase(e->graphs.begin() + lru);  // destroyed now, or by its last replaying caller
-      }
-      e->graphs.push_back(ne);
-      e->n_captures++;
-      hold = ne;
-    }
-    hold->stamp = ++e->use_ctr;
-    e->n_replays += c.nfe;
-  }
+  RC(graph_get(c, key, split, [&](Ctx& cc) { return enqueue_step(cc, a); }, hold, c.nfe));
   for (int k = 0; k < c.nfe; ++k) HIPCK(hipGraphLaunch(hold->exec, c.st));
+  return 0;
+}
+
+// The cached graph for `key`, captured from `body` on the private capture stream(s) when absent.
+static int graph_get(Ctx& c, const GraphKey& key, bool split, const std::function<int(Ctx&)>& body,
+                     std::shared_ptr<GraphEntry>& hold, int64_t replays) {
+  f5h_engine* e = c.e;
+  std::lock_guard<std::mutex> g(e->gm);
+  for (const auto& x : e->graphs)
+    if (x->key == key) hold = x;
+  if (!hold) {
+    if (!e->cap) HIPCK(hipStreamCreateWithFlags(&e->cap, hipStreamNonBlocking));
+    if (split && !e->cap2) {
+      HIPCK(hipStreamCreateWithFlags(&e->cap2, hipStreamNonBlocking));
+      HIPCK(hipEventCreateWithFlags(&e->ev_fork, hipEventDisableTiming));
+      HIPCK(hipEventCreateWithFlags(&e->ev_join, hipEventDisableTiming));
+    }
+    auto ne = std::make_shared<GraphEntry>();
+    ne->key = key;
+    Ctx cc = c;
+    cc.st = e->cap;
+    cc.st2 = split ? e->cap2 : nullptr;
+    hipError_t be = hipStreamBeginCapture(e->cap, hipStreamCaptureModeThreadLocal);
+    if (be != hipSuccess) return fail(F5H_EHIP, std::string("hipStreamBeginCapture: ") + hipGetErrorString(be));
+    const int rc = body(cc);
+    hipGraph_t graph = nullptr;
+    const hipError_t ce = hipStreamEndCapture(e->cap, &graph);
+    if (rc || ce != hipSuccess) {
+      if (graph) (void)hipGraphDestroy(graph);
+      if (rc) return rc;
+      return fail(F5H_EHIP, std::string("hipStreamEndCapture: ") + hipGetErrorString(ce));
+    }
+    const hipError_t ie = hipGraphInstantiate(&ne->exec, graph, nullptr, nullptr, 0);
+    (void)hipGraphDestroy(graph);
+    if (ie != hipSuccess) {
+      ne->exec = nullptr;
+      return fail(F5H_EHIP, std::string("hipGraphInstantiate: ") + hipGetErrorString(ie));
+    }
+    if (e->graphs.size() >= 16) {  // evict the least recently used graph
+      size_t lru = 0;
+      for (size_t i = 1; i < e->graphs.size(); ++i)
+        if (e->graphs[i]->stamp < e->graphs[lru]->stamp) lru = i;
+      e->graphs.erase(e->graphs.begin() + lru);  // destroyed now, or by its last replaying caller
+    }
+    e->graphs.push_back(ne);
+    e->n_captures++;
+    hold = ne;
+  }
+  hold->stamp = ++e->use_ctr;
+  e->n_replays += replays;
   return 0;
 }
 

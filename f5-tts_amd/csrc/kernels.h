@@ -87,6 +87,7 @@ hipError_t conv_pos(int compute, const ConvArgs& a, hipStream_t st);
 
 // ---- elementwise / small kernels (elementwise.hip)
 hipError_t time_sinus(const float* t_host, int n, float* out, hipStream_t st);  // host t[n<=512] -> [n,256]
+hipError_t time_sinus_dev(const float* tg, int n, float* out, hipStream_t st);  // device t[n]
 hipError_t silu_to_op(int compute, const float* x, void* y, int64_t n, hipStream_t st);
 // LayerNorm(no affine, eps) * (1 + scale) + shift -> operand dtype; h: [M, d] fp32, or the operand
 // dtype when h16 (the 16-bit residual stream of the bf16/fp16 DiT path)
