@@ -94,6 +94,44 @@ def cpu_model():
     return "unknown"
 
 
+def host_cores():
+    """Physical cores of the host, and the physical cores this process may run on: the CPUs of its
+    affinity mask counted once per (package, core) from /proc/cpuinfo, capped by a cgroup v2 CPU
+    quota when one is set. The CPU baseline runs one thread per usable physical core."""
+    phys, cpu_core = set(), {}
+    try:
+        cur = {}
+        for line in open("/proc/cpuinfo"):
+            if ":" in line:
+                k, v = (x.strip() for x in line.split(":", 1))
+                cur[k] = v
+            elif cur:
+                if "processor" in cur:
+                    key = (cur.get("physical id", "0"), cur.get("core id", cur["processor"]))
+                    phys.add(key)
+                    cpu_core[int(cur["processor"])] = key
+                cur = {}
+        if cur and "processor" in cur:
+            key = (cur.get("physical id", "0"), cur.get("core id", cur["processor"]))
+            phys.add(key)
+            cpu_core[int(cur["processor"])] = key
+    except OSError:
+        pass
+    aff = os.sched_getaffinity(0) if hasattr(os, "sched_getaffinity") else set(range(os.cpu_count() or 1))
+    usable = len({cpu_core.get(c, ("?", c)) for c in aff}) if cpu_core else len(aff)
+    quota = None
+    try:
+        q, period = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = max(1, int(int(q) // int(period)))
+    except (OSError, ValueError):
+        pass
+    if quota is not None:
+        usable = min(usable, quota)
+    return {"physical": len(phys) or (os.cpu_count() or 1), "usable": max(1, usable), "affinity_cpus": len(aff),
+            "cgroup_cpus": quota}
+
+
 def cpu_baseline(case, arch, threads):
     """Oracle (fp32 PyTorch-CPU restatement of the reference path) timed on the host cores: one full
     16-step C2 CFM.sample call (text embedding, 16 packed CFG forwards, Euler, final overwrite)."""
@@ -110,7 +148,8 @@ def cpu_baseline(case, arch, threads):
     gen = case["total"] - case["ref"]
     return {"value": round(gen / full, 3), "unit": "mel-frames/s", "cores": torch.get_num_threads(), "kind": "port",
             "sample": f"oracle/ref_cpu.py fp32, one full 16-step C2 call ({full:.1f}s, {gen} generated frames) "
-                      f"on {cpu_model()}, {torch.get_num_threads()} threads",
+                      f"on {cpu_model()}, {torch.get_num_threads()} threads (one per physical core usable "
+                      f"by this process)",
             "rtf": round(full / (gen * HOP / SR), 4), "seconds": round(full, 2)}
 
 
@@ -347,7 +386,9 @@ def main():
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline and args.config == "c2":
-        cpu = cpu_baseline(case, arch, threads=min(16, os.cpu_count() or 1))
+        hc = host_cores()
+        cpu = cpu_baseline(case, arch, threads=hc["usable"])
+        cpu["host_cores"] = hc
 
     # whole-path algorithmic FLOPs: NFE * S * F(N) at the padded length, per rank
     flops_call = case["nfe"] * S * seq_flops(arch, Nmax) * len(batches)

@@ -3,6 +3,8 @@
 #include "common.h"
 #include "kernels.h"
 
+#include <algorithm>
+
 namespace f5h {
 
 static inline unsigned nblk(int64_t n, int t) { return (unsigned)((n + t - 1) / t); }
@@ -256,13 +258,13 @@ hipError_t ln_modulate(int compute, const void* hv, int h16, int M, int d, const
 }
 
 // x_transformers RMSNorm: F.normalize(x, dim=-1) * sqrt(d) * g (unett.py:156,160,185)
-template <typename TO, int NV>
-__global__ __launch_bounds__(256) void rms_kernel(const float* h, int M, int d, const float* g, TO* out) {
+template <typename TO, int NV, typename TI = float>
+__global__ __launch_bounds__(256) void rms_kernel(const TI* h, int M, int d, const float* g, TO* out) {
   constexpr bool FIXED = NV > 0;
   constexpr int V = FIXED ? NV : MAXV;
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
   if (row >= M) return;
-  const float4* x = reinterpret_cast<const float4*>(h + (int64_t)row * d);
+  const TI* x = h + (int64_t)row * d;
   const float4* gg = reinterpret_cast<const float4*>(g);
   const int n4 = FIXED ? 64 * NV : d >> 2;
   float4 v[V], a[V];
@@ -271,7 +273,7 @@ __global__ __launch_bounds__(256) void rms_kernel(const float* h, int M, int d, 
   for (int k = 0; k < V; ++k) {
     const int i = lane + 64 * k;
     const bool ok = FIXED || i < n4;
-    v[k] = ok ? x[i] : make_float4(0, 0, 0, 0);
+    v[k] = ok ? load4f<TI>(x + 4 * i) : make_float4(0, 0, 0, 0);
     a[k] = ok ? gg[i] : make_float4(0, 0, 0, 0);
   }
 #pragma unroll
@@ -286,9 +288,27 @@ __global__ __launch_bounds__(256) void rms_kernel(const float* h, int M, int d, 
                  v[k].z / nrm * f * a[k].z, v[k].w / nrm * f * a[k].w);
   }
 }
-hipError_t rms_norm_g(int compute, const float* h, int M, int d, const float* g, void* out, hipStream_t st) {
+hipError_t rms_norm_g(int compute, const void* hv, int h16, int M, int d, const float* g, void* out, hipStream_t st) {
   if (d % 4 || d > 4 * 64 * MAXV) return hipErrorInvalidValue;
   const dim3 gr(nblk(M, 4)), b(256);
+  if (h16) {  // 16-bit residual stream (UNetT in the 16-bit modes): input and output in the operand dtype
+    if (compute != F5H_C_BF16 && compute != F5H_C_FP16) return hipErrorInvalidValue;
+    auto run = [&](auto tag) {
+      typedef decltype(tag) T;
+      const T* x = (const T*)hv;
+      switch (d) {
+        case 1024: hipLaunchKernelGGL((rms_kernel<T, 4, T>), gr, b, 0, st, x, M, d, g, (T*)out); break;
+        case 512: hipLaunchKernelGGL((rms_kernel<T, 2, T>), gr, b, 0, st, x, M, d, g, (T*)out); break;
+        default: hipLaunchKernelGGL((rms_kernel<T, 0, T>), gr, b, 0, st, x, M, d, g, (T*)out);
+      }
+    };
+    if (compute == F5H_C_BF16)
+      run(bf16{});
+    else
+      run(f16{});
+    return hipGetLastError();
+  }
+  const float* h = (const float*)hv;
   switch (d) {
     case 1024: F5H_OP_DISPATCH(compute, T, hipLaunchKernelGGL((rms_kernel<T, 4>), gr, b, 0, st, h, M, d, g, (T*)out);); break;
     case 512: F5H_OP_DISPATCH(compute, T, hipLaunchKernelGGL((rms_kernel<T, 2>), gr, b, 0, st, h, M, d, g, (T*)out);); break;
@@ -581,14 +601,23 @@ hipError_t build_kvlen(const int32_t* dur, int B, int S, int off, int32_t* kv, h
   return hipGetLastError();
 }
 
-__global__ void time_token_kernel(const float* temb, int S, int L, int d, float* h) {
+template <typename TH>
+__global__ void time_token_kernel(const float* temb, int S, int L, int d, TH* h) {
   int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= (int64_t)S * d) return;
   int s = (int)(i / d), c = (int)(i % d);
-  h[(int64_t)s * L * d + c] = temb[c];
+  h[(int64_t)s * L * d + c] = from_f32<TH>(temb[c]);
 }
-hipError_t write_time_token(const float* temb, int S, int L, int d, float* h, hipStream_t st) {
-  hipLaunchKernelGGL(time_token_kernel, dim3(nblk((int64_t)S * d, 256)), dim3(256), 0, st, temb, S, L, d, h);
+hipError_t write_time_token(int compute, int h16, const float* temb, int S, int L, int d, void* h, hipStream_t st) {
+  const dim3 g(nblk((int64_t)S * d, 256)), b(256);
+  if (!h16)
+    hipLaunchKernelGGL(time_token_kernel<float>, g, b, 0, st, temb, S, L, d, (float*)h);
+  else if (compute == F5H_C_BF16)
+    hipLaunchKernelGGL(time_token_kernel<bf16>, g, b, 0, st, temb, S, L, d, (bf16*)h);
+  else if (compute == F5H_C_FP16)
+    hipLaunchKernelGGL(time_token_kernel<f16>, g, b, 0, st, temb, S, L, d, (f16*)h);
+  else
+    return hipErrorInvalidValue;
   return hipGetLastError();
 }
 
@@ -623,6 +652,46 @@ hipError_t f32_to_op(int compute, const float* x, int64_t n, void* out, hipStrea
 }
 hipError_t op_to_f32(int compute, const void* x, int64_t n, float* out, hipStream_t st) {
   F5H_OP_DISPATCH(compute, T, hipLaunchKernelGGL(cvt_back_kernel<T>, dim3(nblk(n, 256)), dim3(256), 0, st, (const T*)x, n, out););
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------- weight packing
+template <typename T> F5H_DEV float ld_elem(const void* p, int64_t i) { return to_f32(reinterpret_cast<const T*>(p)[i]); }
+__global__ __launch_bounds__(256) void pack_strided_kernel(PackArgs a, int64_t total) {
+  for (int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x; t < total; t += (int64_t)gridDim.x * 256) {
+    int64_t r = t;
+    const int i3 = (int)(r % a.n[3]);
+    r /= a.n[3];
+    const int i2 = (int)(r % a.n[2]);
+    r /= a.n[2];
+    const int i1 = (int)(r % a.n[1]);
+    const int i0 = (int)(r / a.n[1]);
+    const int64_t si = i0 * a.src_st[0] + i1 * a.src_st[1] + i2 * a.src_st[2] + i3 * a.src_st[3];
+    const int64_t di = i0 * a.dst_st[0] + i1 * a.dst_st[1] + i2 * a.dst_st[2] + i3;
+    if (a.src_dt == 1 && a.dst_dt == 1) {  // same 16-bit type: bit copy
+      reinterpret_cast<uint16_t*>(a.dst)[di] = reinterpret_cast<const uint16_t*>(a.src)[si];
+      continue;
+    }
+    if (a.src_dt == 2 && a.dst_dt == 2) {
+      reinterpret_cast<uint16_t*>(a.dst)[di] = reinterpret_cast<const uint16_t*>(a.src)[si];
+      continue;
+    }
+    const float v = a.src_dt == 0 ? ld_elem<float>(a.src, si) : (a.src_dt == 1 ? ld_elem<bf16>(a.src, si)
+                                                                                 : ld_elem<f16>(a.src, si));
+    if (a.dst_dt == 0)
+      reinterpret_cast<float*>(a.dst)[di] = v;
+    else if (a.dst_dt == 1)
+      reinterpret_cast<bf16*>(a.dst)[di] = f2bf(v);
+    else
+      reinterpret_cast<f16*>(a.dst)[di] = (f16)v;
+  }
+}
+hipError_t pack_strided(const PackArgs& a, hipStream_t st) {
+  const int64_t total = (int64_t)a.n[0] * a.n[1] * a.n[2] * a.n[3];
+  if (total <= 0) return hipSuccess;
+  if (a.src_dt < 0 || a.src_dt > 2 || a.dst_dt < 0 || a.dst_dt > 2) return hipErrorInvalidValue;
+  const int64_t blocks = std::min<int64_t>((total + 255) / 256, 65536);
+  hipLaunchKernelGGL(pack_strided_kernel, dim3((unsigned)blocks), dim3(256), 0, st, a, total);
   return hipGetLastError();
 }
 

@@ -48,21 +48,6 @@ int f5h_internal_fail(int code, const std::string& msg) { return fail(code, msg)
     if (_r) return _r;     \
   } while (0)
 
-static uint16_t f2bf_host(float f) {
-  uint32_t u;
-  std::memcpy(&u, &f, 4);
-  if ((u & 0x7fffffffu) > 0x7f800000u) return (uint16_t)((u >> 16) | 0x40);
-  u += 0x7fffu + ((u >> 16) & 1u);
-  return (uint16_t)(u >> 16);
-}
-
-static uint16_t f2h_host(float f) {  // round-to-nearest-even fp32 -> fp16 (clang _Float16 on the host)
-  _Float16 h = (_Float16)f;
-  uint16_t u;
-  std::memcpy(&u, &h, 2);
-  return u;
-}
-
 struct Lin {
   void* w = nullptr;      // [Npad][K] operand dtype
   float* b = nullptr;     // [Npad] fp32 (may be null)
@@ -75,8 +60,21 @@ struct CNX {
 };
 
 struct Layer {
-  Lin qkv, out, ff1, ff2, skip1, skip2;
+  Lin qkv, out, ff1, ff2, skip;  // skip: UNetT skip_proj [d][2d] over cat(x, skip) (later half)
   float *g_attn = nullptr, *g_ff = nullptr;  // UNetT RMSNorm gains
+};
+
+struct GraphKey {
+  const void* ws;
+  int kind;  // 0: one NFE step, 1: the call prologue (inputs staged into the workspace)
+  int B, N, nt, nfe, use_cfg, batch_mask, probe, split;
+  uint64_t kernel_epoch;  // bumped whenever a forced GEMM config changes
+  uint32_t cfg_bits;
+  bool operator==(const GraphKey& o) const {
+    return ws == o.ws && kind == o.kind && B == o.B && N == o.N && nt == o.nt && nfe == o.nfe && kernel_epoch == o.kernel_epoch &&
+           use_cfg == o.use_cfg && batch_mask == o.batch_mask && probe == o.probe && cfg_bits == o.cfg_bits &&
+           split == o.split;
+  }
 };
 
 struct f5h_engine {
@@ -97,6 +95,14 @@ struct f5h_engine {
   // hipGraph cache of one NFE step (keyed by the call's buffers and shape)
   std::mutex gm;
   std::vector<std::shared_ptr<struct GraphEntry>> graphs;
+  // evicted entries whose replays may still be in flight: destroyed by a later graph_get once every
+  // event recorded after their replays has completed and no caller holds them (no host wait)
+  std::vector<std::shared_ptr<struct GraphEntry>> graveyard;
+  std::vector<hipEvent_t> ev_pool;  // completed "replays done" events, reused
+  // prologue keys seen once: the prologue is captured only when its shape repeats (a call with a
+  // new shape runs it eagerly instead of paying capture + instantiate for one replay)
+  std::vector<struct GraphKey> pro_seen;
+  int64_t n_evicted = 0, n_reaped = 0;
   hipStream_t cap = nullptr;  // private capture stream (the caller's may be the null stream)
   hipStream_t cap2 = nullptr; // second capture stream: the unconditional CFG branch
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;
@@ -120,6 +126,7 @@ struct f5h_engine {
   int* ptick = nullptr;
   double wall_khz = 0.0;
 };
+static constexpr size_t kGraphCache = 16;  // cached graphs (prologue and step graphs together)
 static constexpr size_t kProbeBytes = (64 + 2 * (size_t)kProbeEnd) * sizeof(unsigned long long);
 
 // The step graph touches only workspace buffers (the ODE state, the trajectory base and the step
@@ -128,18 +135,6 @@ static constexpr size_t kProbeBytes = (64 + 2 * (size_t)kProbeEnd) * sizeof(unsi
 // (tuning/tests) moves the epoch so that later calls capture afresh.
 static std::atomic<uint64_t> g_kernel_epoch{0};
 
-struct GraphKey {
-  const void* ws;
-  int kind;  // 0: one NFE step, 1: the call prologue (inputs staged into the workspace)
-  int B, N, nt, nfe, use_cfg, batch_mask, probe, split;
-  uint64_t kernel_epoch;  // bumped whenever a forced GEMM config changes
-  uint32_t cfg_bits;
-  bool operator==(const GraphKey& o) const {
-    return ws == o.ws && kind == o.kind && B == o.B && N == o.N && nt == o.nt && nfe == o.nfe && kernel_epoch == o.kernel_epoch &&
-           use_cfg == o.use_cfg && batch_mask == o.batch_mask && probe == o.probe && cfg_bits == o.cfg_bits &&
-           split == o.split;
-  }
-};
 // Shared by the cache and by every call replaying it: an entry evicted while another thread is
 // still in its launch loop is destroyed by the last holder, after the device has drained (an
 // already-submitted replay may still be executing).
@@ -147,29 +142,39 @@ struct GraphEntry {
   GraphKey key{};
   hipGraphExec_t exec = nullptr;
   uint64_t stamp = 0;
+  std::vector<hipEvent_t> inflight;  // recorded after this entry's replays (guarded by f5h_engine::gm)
+  // Destroyed only when nothing replays it any more: from the graveyard once `inflight` has
+  // completed and no caller holds it, or by f5h_engine_destroy after a device synchronisation.
   ~GraphEntry() {
-    if (exec) {
-      (void)hipDeviceSynchronize();
-      (void)hipGraphExecDestroy(exec);
-    }
+    if (exec) (void)hipGraphExecDestroy(exec);
+    for (hipEvent_t ev : inflight) (void)hipEventDestroy(ev);
   }
 };
 
 // ---------------------------------------------------------------- weight packing
+// Weights arrive as typed views (f5h_tensor_view: fp32/bf16/fp16, host or device memory, the
+// reference's parameter dtype and placement, utils_infer.py:190-232). Host views are staged to the
+// device once in their own dtype; every panel is then packed on the device by pack_strided
+// (reorder, zero padding, rounding to the operand dtype), so no host fp32 copy of the model exists.
+struct WView {
+  const void* p;      // device pointer (staged when the caller's view was in host memory)
+  int dt;             // f5h_dtype
+  int64_t numel;
+};
 struct WMap {
-  std::unordered_map<std::string, std::pair<const float*, int64_t>> m;
-  const float* get(const std::string& n, int64_t numel, std::string* err) const {
+  std::unordered_map<std::string, WView> m;
+  const WView* get(const std::string& n, int64_t numel, std::string* err) const {
     auto it = m.find(n);
     if (it == m.end()) {
       *err = "missing weight " + n;
       return nullptr;
     }
-    if (it->second.second != numel) {
-      *err = "weight " + n + " has " + std::to_string(it->second.second) + " elements, expected " +
+    if (it->second.numel != numel) {
+      *err = "weight " + n + " has " + std::to_string(it->second.numel) + " elements, expected " +
              std::to_string(numel);
       return nullptr;
     }
-    return it->second.first;
+    return &it->second;
   }
 };
 
@@ -183,86 +188,100 @@ static int upload(f5h_engine* e, const std::vector<T>& h, T** out) {
   return 0;
 }
 
-static int upload_op(f5h_engine* e, const std::vector<float>& h, void** out) {
-  if (e->bf) {
-    std::vector<uint16_t> b(h.size());
-    if (e->bf == F5H_FP16)
-      for (size_t i = 0; i < h.size(); ++i) b[i] = f2h_host(h[i]);
-    else
-      for (size_t i = 0; i < h.size(); ++i) b[i] = f2bf_host(h[i]);
-    uint16_t* p;
-    int rc = upload(e, b, &p);
-    *out = p;
-    return rc;
-  }
-  float* p;
-  int rc = upload(e, h, &p);
+// zeroed device buffer owned by the engine
+static int dalloc(f5h_engine* e, size_t bytes, void** out) {
+  void* p = nullptr;
+  HIPCK(hipMalloc(&p, bytes + 16));
+  e->allocs.push_back(p);
+  HIPCK(hipMemset(p, 0, bytes + 16));
   *out = p;
-  return rc;
-}
-
-// Upload a host panel [Npad][K] (+ optional bias [N]) as a GEMM weight.
-static int lin_from_host(f5h_engine* e, const std::vector<float>& w, int N, int K, const std::vector<float>* bias,
-                         Lin* L) {
-  L->N = N;
-  L->K = K;
-  L->Npad = (N + 127) / 128 * 128;
-  RC(upload_op(e, w, &L->w));
-  if (bias) {
-    std::vector<float> bv(L->Npad, 0.f);
-    std::copy(bias->begin(), bias->end(), bv.begin());
-    RC(upload(e, bv, &L->b));
-  }
   return 0;
 }
 
-// Build a GEMM panel from column blocks of several source matrices stacked along N.
+// op element type of the engine (f5h_dtype numbering: 0 fp32, 1 bf16, 2 fp16 == f5h_compute)
+static int op_dt(const f5h_engine* e) { return e->bf; }
+
+// dst[r][dst_col + c] (row stride ld_dst, element type ddt) = src[r][col0 + c] (row stride ld_src)
+static int pack_rows(const WView& v, int rows, int64_t ld_src, int col0, int ncols, void* dst, int ddt,
+                     int64_t ld_dst, int dst_row0, int dst_col) {
+  PackArgs pa{};
+  pa.src = v.p;
+  pa.src_dt = v.dt;
+  pa.src_st[0] = 0;
+  pa.src_st[1] = 0;
+  pa.src_st[2] = ld_src;
+  pa.src_st[3] = 1;
+  const size_t esz = ddt ? 2 : 4;
+  pa.dst = (char*)dst + ((size_t)dst_row0 * ld_dst + dst_col) * esz;
+  // the source column offset goes into the base pointer
+  pa.src = (const char*)v.p + (size_t)col0 * (v.dt ? 2 : 4);
+  pa.dst_dt = ddt;
+  pa.dst_st[0] = 0;
+  pa.dst_st[1] = 0;
+  pa.dst_st[2] = ld_dst;
+  pa.n[0] = 1;
+  pa.n[1] = 1;
+  pa.n[2] = rows;
+  pa.n[3] = ncols;
+  HIPCK(pack_strided(pa, nullptr));
+  return 0;
+}
+
+// Build a GEMM panel [Npad][K] (operand dtype, zero padded) from column blocks of several source
+// matrices stacked along N, plus an fp32 bias [Npad] from per-block bias vectors (null: zeros).
 struct Block {
-  const float* src;   // [rows][ld]
+  const WView* src;   // [rows][ld]
   int rows, ld, col0, ncols, dst_col;
 };
-static int make_lin(f5h_engine* e, const std::vector<Block>& blocks, int K, const std::vector<const float*>& biases,
-                    const std::vector<int>& bias_rows, Lin* L) {
+static int make_lin(f5h_engine* e, const std::vector<Block>& blocks, int K, const std::vector<const WView*>& biases,
+                    Lin* L) {
   int N = 0;
-  std::vector<int> row0(blocks.size());
-  for (size_t i = 0; i < blocks.size(); ++i) {
-    row0[i] = N;
-    N += blocks[i].rows;
+  for (const Block& b : blocks) N += b.rows;
+  L->N = N;
+  L->K = K;
+  L->Npad = (N + 127) / 128 * 128;
+  RC(dalloc(e, (size_t)L->Npad * K * e->esz, &L->w));
+  int r0 = 0;
+  for (const Block& b : blocks) {
+    RC(pack_rows(*b.src, b.rows, b.ld, b.col0, b.ncols, L->w, op_dt(e), K, r0, b.dst_col));
+    r0 += b.rows;
   }
-  const int Npad = (N + 127) / 128 * 128;
-  std::vector<float> w((size_t)Npad * K, 0.f);
-  for (size_t i = 0; i < blocks.size(); ++i) {
-    const Block& b = blocks[i];
-    for (int r = 0; r < b.rows; ++r)
-      for (int c = 0; c < b.ncols; ++c)
-        w[(size_t)(row0[i] + r) * K + b.dst_col + c] = b.src[(size_t)r * b.ld + b.col0 + c];
+  if (!biases.empty()) {
+    void* bp;
+    RC(dalloc(e, (size_t)L->Npad * sizeof(float), &bp));
+    L->b = reinterpret_cast<float*>(bp);
+    r0 = 0;
+    for (size_t i = 0; i < blocks.size(); ++i) {
+      if (i < biases.size() && biases[i]) RC(pack_rows(*biases[i], 1, 0, 0, blocks[i].rows, L->b, 0, 0, 0, r0));
+      r0 += blocks[i].rows;
+    }
   }
-  if (biases.empty()) return lin_from_host(e, w, N, K, nullptr, L);
-  std::vector<float> bv;
-  for (size_t i = 0; i < biases.size(); ++i)
-    for (int r = 0; r < bias_rows[i]; ++r) bv.push_back(biases[i] ? biases[i][r] : 0.f);
-  return lin_from_host(e, w, N, K, &bv, L);
+  return 0;
 }
-// Simple linear: weight [N][K] (K padded to Kp), bias [N] or null.
+// Simple linear: weight [N][K] (K padded to 64), bias [N] or none.
 static int lin_simple(f5h_engine* e, const WMap& W, const std::string& wn, const std::string& bn, int N, int K,
                       Lin* L, std::string* err) {
-  const float* w = W.get(wn, (int64_t)N * K, err);
+  const WView* w = W.get(wn, (int64_t)N * K, err);
   if (!w) return fail(F5H_ENOWEIGHT, *err);
-  const float* b = nullptr;
+  const WView* b = nullptr;
   if (!bn.empty()) {
     b = W.get(bn, N, err);
     if (!b) return fail(F5H_ENOWEIGHT, *err);
   }
   const int Kp = (K + 63) / 64 * 64;
-  return make_lin(e, {Block{w, N, K, 0, K, 0}}, Kp, b ? std::vector<const float*>{b} : std::vector<const float*>{},
-                  std::vector<int>{N}, L);
+  return make_lin(e, {Block{w, N, K, 0, K, 0}}, Kp, b ? std::vector<const WView*>{b} : std::vector<const WView*>{},
+                  L);
 }
+// fp32 device copy of a vector parameter
 static int vec_upload(f5h_engine* e, const WMap& W, const std::string& n, int64_t numel, float** out, std::string* err) {
-  const float* p = W.get(n, numel, err);
-  if (!p) return fail(F5H_ENOWEIGHT, *err);
-  return upload(e, std::vector<float>(p, p + numel), out);
+  const WView* v = W.get(n, numel, err);
+  if (!v) return fail(F5H_ENOWEIGHT, *err);
+  void* p;
+  RC(dalloc(e, (size_t)numel * sizeof(float), &p));
+  RC(pack_rows(*v, 1, 0, 0, (int)numel, p, 0, 0, 0, 0));
+  *out = reinterpret_cast<float*>(p);
+  return 0;
 }
-
 
 static int pack_all(f5h_engine* e, const WMap& W) {
   const f5h_arch& a = e->a;
@@ -303,82 +322,96 @@ static int pack_all(f5h_engine* e, const WMap& W) {
   // input projection split (dit.py:162): [x | cond | text] -> x part per step, cond|text hoisted
   {
     const int Kin = 2 * mel + td;
-    const float* w = W.get("input_embed.proj.weight", (int64_t)d * Kin, &err);
-    const float* b = W.get("input_embed.proj.bias", d, &err);
+    const WView* w = W.get("input_embed.proj.weight", (int64_t)d * Kin, &err);
+    const WView* b = w ? W.get("input_embed.proj.bias", d, &err) : nullptr;
     if (!w || !b) return fail(F5H_ENOWEIGHT, err);
-    RC(make_lin(e, {Block{w, d, Kin, 0, mel, 0}}, 128, {}, {d}, &e->in_x));
-    // cond columns -> [0,128), text columns -> [128, 128+tdp)
+    RC(make_lin(e, {Block{w, d, Kin, 0, mel, 0}}, 128, {}, &e->in_x));
+    // cond columns -> [0,128), text columns -> [128, 128+tdp): two column blocks of the same rows
     const int Kct = 128 + e->tdp;
-    std::vector<float> tmp((size_t)((d + 127) / 128 * 128) * Kct, 0.f);
-    for (int r = 0; r < d; ++r) {
-      for (int c = 0; c < mel; ++c) tmp[(size_t)r * Kct + c] = w[(size_t)r * Kin + mel + c];
-      for (int c = 0; c < td; ++c) tmp[(size_t)r * Kct + 128 + c] = w[(size_t)r * Kin + 2 * mel + c];
-    }
-    std::vector<float> bv(b, b + d);
-    RC(lin_from_host(e, tmp, d, Kct, &bv, &e->in_ct));
+    Lin& L = e->in_ct;
+    L.N = d;
+    L.K = Kct;
+    L.Npad = (d + 127) / 128 * 128;
+    RC(dalloc(e, (size_t)L.Npad * Kct * e->esz, &L.w));
+    RC(pack_rows(*w, d, Kin, mel, mel, L.w, op_dt(e), Kct, 0, 0));
+    RC(pack_rows(*w, d, Kin, 2 * mel, td, L.w, op_dt(e), Kct, 0, 128));
+    void* bp;
+    RC(dalloc(e, (size_t)L.Npad * sizeof(float), &bp));
+    L.b = reinterpret_cast<float*>(bp);
+    RC(pack_rows(*b, 1, 0, 0, d, L.b, 0, 0, 0, 0));
   }
-  // ConvPositionEmbedding: [d, d/16, 31] -> [16][31][64 out][64 in] (zero-padded to 64 channels)
+  // ConvPositionEmbedding: [d, d/16, 31] -> [16][31][64 out][64 in] (zero-padded to 64 channels):
+  // dst (g, t, o, i) <- src ((g*cg + o)*cg + i)*31 + t
   for (int j = 0; j < 2; ++j) {
     const std::string p = "input_embed.conv_pos_embed.conv1d." + std::to_string(j * 2) + ".";
     const int cg = d / 16;
-    const float* w = W.get(p + "weight", (int64_t)d * cg * 31, &err);
+    const WView* w = W.get(p + "weight", (int64_t)d * cg * 31, &err);
     if (!w) return fail(F5H_ENOWEIGHT, err);
-    std::vector<float> pk((size_t)16 * 31 * 64 * 64, 0.f);
-    for (int g = 0; g < 16; ++g)
-      for (int o = 0; o < cg; ++o)
-        for (int i = 0; i < cg; ++i)
-          for (int t = 0; t < 31; ++t)
-            pk[(((size_t)g * 31 + t) * 64 + o) * 64 + i] = w[((size_t)(g * cg + o) * cg + i) * 31 + t];
-    RC(upload_op(e, pk, &e->conv_w[j]));
+    RC(dalloc(e, (size_t)16 * 31 * 64 * 64 * e->esz, &e->conv_w[j]));
+    PackArgs pa{};
+    pa.src = w->p;
+    pa.src_dt = w->dt;
+    pa.src_st[0] = (int64_t)cg * cg * 31;  // g
+    pa.src_st[1] = 1;                      // t
+    pa.src_st[2] = (int64_t)cg * 31;       // o
+    pa.src_st[3] = 31;                     // i
+    pa.dst = e->conv_w[j];
+    pa.dst_dt = op_dt(e);
+    pa.dst_st[0] = 31 * 64 * 64;
+    pa.dst_st[1] = 64 * 64;
+    pa.dst_st[2] = 64;
+    pa.n[0] = 16;
+    pa.n[1] = 31;
+    pa.n[2] = cg;
+    pa.n[3] = cg;
+    HIPCK(pack_strided(pa, nullptr));
     RC(vec_upload(e, W, p + "bias", d, &e->conv_b[j], &err));
   }
   // blocks
   e->layers.resize(a.depth);
   std::vector<Block> ada_blocks;
-  std::vector<const float*> ada_bias;
-  std::vector<int> ada_rows;
+  std::vector<const WView*> ada_bias;
   for (int l = 0; l < a.depth; ++l) {
     Layer& L = e->layers[l];
     const bool dit = a.backbone == F5H_DIT;
     const std::string p = dit ? "transformer_blocks." + std::to_string(l) + "." : "layers." + std::to_string(l) + ".";
     const std::string pa = dit ? p + "attn." : p + "2.";
     const std::string pf = dit ? p + "ff.ff." : p + "4.ff.";
-    const float *wq = W.get(pa + "to_q.weight", (int64_t)inner * d, &err), *wk = W.get(pa + "to_k.weight", (int64_t)inner * d, &err),
-                *wv = W.get(pa + "to_v.weight", (int64_t)inner * d, &err);
-    const float *bq = W.get(pa + "to_q.bias", inner, &err), *bk = W.get(pa + "to_k.bias", inner, &err),
-                *bv = W.get(pa + "to_v.bias", inner, &err);
+    const WView* wq = W.get(pa + "to_q.weight", (int64_t)inner * d, &err);
+    const WView* wk = wq ? W.get(pa + "to_k.weight", (int64_t)inner * d, &err) : nullptr;
+    const WView* wv = wk ? W.get(pa + "to_v.weight", (int64_t)inner * d, &err) : nullptr;
+    const WView* bq = wv ? W.get(pa + "to_q.bias", inner, &err) : nullptr;
+    const WView* bk = bq ? W.get(pa + "to_k.bias", inner, &err) : nullptr;
+    const WView* bv = bk ? W.get(pa + "to_v.bias", inner, &err) : nullptr;
     if (!wq || !wk || !wv || !bq || !bk || !bv) return fail(F5H_ENOWEIGHT, err);
     RC(make_lin(e, {Block{wq, inner, d, 0, d, 0}, Block{wk, inner, d, 0, d, 0}, Block{wv, inner, d, 0, d, 0}}, d,
-                {bq, bk, bv}, {inner, inner, inner}, &L.qkv));
+                {bq, bk, bv}, &L.qkv));
     RC(lin_simple(e, W, pa + "to_out.0.weight", pa + "to_out.0.bias", d, inner, &L.out, &err));
     RC(lin_simple(e, W, pf + "0.0.weight", pf + "0.0.bias", F, d, &L.ff1, &err));
     RC(lin_simple(e, W, pf + "2.weight", pf + "2.bias", d, F, &L.ff2, &err));
     if (dit) {
-      const float* aw = W.get(p + "attn_norm.linear.weight", (int64_t)6 * d * d, &err);
-      const float* ab = W.get(p + "attn_norm.linear.bias", 6 * d, &err);
+      const WView* aw = W.get(p + "attn_norm.linear.weight", (int64_t)6 * d * d, &err);
+      const WView* ab = aw ? W.get(p + "attn_norm.linear.bias", 6 * d, &err) : nullptr;
       if (!aw || !ab) return fail(F5H_ENOWEIGHT, err);
       ada_blocks.push_back(Block{aw, 6 * d, d, 0, d, 0});
       ada_bias.push_back(ab);
-      ada_rows.push_back(6 * d);
     } else {
       RC(vec_upload(e, W, p + "1.g", d, &L.g_attn, &err));
       RC(vec_upload(e, W, p + "3.g", d, &L.g_ff, &err));
       if (l >= a.depth / 2) {
-        const float* sw = W.get(p + "0.weight", (int64_t)d * 2 * d, &err);
+        const WView* sw = W.get(p + "0.weight", (int64_t)d * 2 * d, &err);
         if (!sw) return fail(F5H_ENOWEIGHT, err);
-        RC(make_lin(e, {Block{sw, d, 2 * d, 0, d, 0}}, d, {}, {d}, &L.skip1));
-        RC(make_lin(e, {Block{sw, d, 2 * d, d, d, 0}}, d, {}, {d}, &L.skip2));
+        RC(make_lin(e, {Block{sw, d, 2 * d, 0, 2 * d, 0}}, 2 * d, {}, &L.skip));
       }
     }
   }
   if (a.backbone == F5H_DIT) {
-    const float* nw = W.get("norm_out.linear.weight", (int64_t)2 * d * d, &err);
-    const float* nb = W.get("norm_out.linear.bias", 2 * d, &err);
+    const WView* nw = W.get("norm_out.linear.weight", (int64_t)2 * d * d, &err);
+    const WView* nb = nw ? W.get("norm_out.linear.bias", 2 * d, &err) : nullptr;
     if (!nw || !nb) return fail(F5H_ENOWEIGHT, err);
     ada_blocks.push_back(Block{nw, 2 * d, d, 0, d, 0});
     ada_bias.push_back(nb);
-    ada_rows.push_back(2 * d);
-    RC(make_lin(e, ada_blocks, d, ada_bias, ada_rows, &e->ada));
+    RC(make_lin(e, ada_blocks, d, ada_bias, &e->ada));
   } else {
     RC(vec_upload(e, W, "norm_out.g", d, &e->norm_out_g, &err));
   }
@@ -407,7 +440,7 @@ struct Bufs {
   void* act;
   float* P;
   void* ypad;
-  float *h0, *h, *h2, *p;
+  float *h0, *h, *p;
   void *c1, *aop, *q, *k, *v, *o, *f;
   float2* rope;
   uint8_t* rowkeep;
@@ -416,7 +449,10 @@ struct Bufs {
   int* kstep;                         // device-side NFE step index
   float* y;                           // ODE state [B][N][mel] fp32
   float** trajp;                      // device slot: trajectory base pointer (or null)
-  std::vector<void*> skips;
+  // UNetT residual stream (operand dtype): xs[0..depth/2] -- layer l < depth/2 reads xs[l] (its
+  // skip connection, kept) and writes xs[l+1]; later layers ping-pong between pp[0] and pp[1]
+  std::vector<void*> xs;
+  void* pp[2];
   // the call's inputs staged into the workspace (prologue graph): cond [B][N][mel] fp32,
   // cond_mask [B][N], text [B][<= N] (int64), duration [B]
   float* in_cond;
@@ -452,8 +488,7 @@ static void layout(const f5h_engine* e, WS& ws, Bufs& b, int B, int N, int nfe, 
   b.ypad = ws.take<char>((size_t)B * N * 128 * es);
   b.h0 = ws.take<float>((size_t)S * N * d);
   b.c1 = ws.take<char>((size_t)S * N * d * es);
-  b.h = ws.take<float>(rows * d);
-  b.h2 = a.backbone == F5H_UNETT ? ws.take<float>(rows * d) : nullptr;
+  b.h = a.backbone == F5H_DIT ? ws.take<float>(rows * d) : nullptr;  // DiT residual stream
   b.aop = ws.take<char>(rows * d * es);
   b.q = ws.take<char>(rows * inner * es);
   b.k = ws.take<char>(rows * inner * es);
@@ -474,9 +509,13 @@ static void layout(const f5h_engine* e, WS& ws, Bufs& b, int B, int N, int nfe, 
   b.in_mask = ws.take<uint8_t>((size_t)B * N);
   b.in_text = ws.take<int64_t>((size_t)B * N);
   b.in_dur = ws.take<int32_t>((size_t)B);
-  b.skips.clear();
-  if (a.backbone == F5H_UNETT)
-    for (int i = 0; i < a.depth / 2; ++i) b.skips.push_back(ws.take<char>(rows * d * es));
+  b.xs.clear();
+  b.pp[0] = b.pp[1] = nullptr;
+  if (a.backbone == F5H_UNETT) {
+    for (int i = 0; i <= a.depth / 2; ++i) b.xs.push_back(ws.take<char>(rows * d * es));
+    b.pp[0] = ws.take<char>(rows * d * es);
+    b.pp[1] = ws.take<char>(rows * d * es);
+  }
 }
 
 // ---------------------------------------------------------------- probe
@@ -541,7 +580,7 @@ static GemmArgs gargs(const void* A, int64_t lda, const Lin& W, int M, void* C, 
 // Everything that depends only on the call's inputs (not on y): time/AdaLN tables, text
 // embedding, hoisted input projection, masks, rope table.
 static int prologue(Ctx& c, const float* t_host, int nt_vals, const float* cond, const uint8_t* cond_mask,
-                    const int64_t* text, const int32_t* duration) {
+                    const int64_t* text, const int32_t* duration, bool text_cached = false) {
   f5h_engine* e = c.e;
   const f5h_arch& a = e->a;
   const int d = a.dim, td = a.text_dim, bf = e->bf;
@@ -571,8 +610,9 @@ static int prologue(Ctx& c, const float* t_host, int nt_vals, const float* cond,
       KCK(gemm(bf, EPI_STORE, g, st));
     }
   }
-  // ---- text embedding, both branches (cached once per call in the reference, dit.py:294-310)
-  {
+  // ---- text embedding, both branches (cached once per call in the reference, dit.py:294-310);
+  // text_cached: the plugin's kept embedding is already in the workspace (f5h_forward text_cache 2)
+  if (!text_cached) {
     TextEmbArgs t{};
     t.text = text;
     t.B = c.B;
@@ -634,16 +674,23 @@ static int backbone_part(Ctx& c, int s0, int ns, hipStream_t st) {
   const size_t no = (size_t)s0 * c.N;  // first row in the N-row input-embedding buffers
   auto op = [&](void* base, size_t row, size_t width) -> void* { return (char*)base + row * width * es; };
   const uint8_t* keep = c.batch_mask ? b.rowkeep + ro : nullptr;
-  // residual stream h: fp32, or the operand dtype on the 16-bit DiT path (as the reference keeps it in
-  // the parameter dtype); UNetT keeps fp32 (its skip connections and time token)
-  static const bool res32 = [] {  // F5H_RES32=1: fp32 residual on the 16-bit path too (A/B)
+  // residual stream: the operand dtype (as the reference keeps it in the parameter dtype), i.e. 16 bit
+  // in the bf16/fp16 modes for DiT and UNetT alike, fp32 in the fp32 parity mode
+  static const bool res32 = [] {  // F5H_RES32=1: fp32 residual on the 16-bit DiT path (A/B)
     const char* v = getenv("F5H_RES32");
     return v && *v == '1';
   }();
-  const bool r16 = bf != 0 && dit && !res32;
+  const bool r16 = bf != 0 && (!dit || !res32);
+  // F5H_DIAG_SKIP_LN=1: timing-only diagnostic, the 16-bit DiT path skips its LayerNorm launches
+  // (wrong results; bounds what removing those launches can save). Never set in tests or benches.
+  static const bool skip_ln = [] {
+    const char* v = getenv("F5H_DIAG_SKIP_LN");
+    return v && *v == '1';
+  }();
+  const bool do_ln = !(skip_ln && r16);
   const size_t hsz = r16 ? es : sizeof(float);
-  void* bh = (char*)b.h + ro * d * hsz;
-  float* bh2 = b.h2 ? b.h2 + ro * d : nullptr;
+  auto res = [&](void* base) -> void* { return (char*)base + ro * d * hsz; };
+  void* bh = dit ? res(b.h) : res(b.xs[0]);
   void* aop = op(b.aop, ro, d);
   void* q = op(b.q, ro, inner);
   void* k = op(b.k, ro, inner);
@@ -685,31 +732,37 @@ static int backbone_part(Ctx& c, int s0, int ns, hipStream_t st) {
     cv.resid = b.h0 + no * d;
     KCK(conv_pos(bf, cv, st));
   }
-  if (!dit) KCK(write_time_token(b.temb_cur, ns, c.L, d, (float*)bh, st));
+  if (!dit) KCK(write_time_token(bf, r16, b.temb_cur, ns, c.L, d, bh, st));
 
   const float* ada_k = dit ? b.ada_cur : nullptr;
   const int epi_resid = r16 ? EPI_RESID16 : EPI_RESID;
-  void* h = bh;
-  void* h2 = bh2;
+  void* h = bh;             // the layer's output (residual updates land here)
+  const void* h_in = nullptr;  // UNetT first half: the layer input, kept as its skip connection
   for (int l = 0; l < a.depth; ++l) {
     Layer& Ly = e->layers[l];
     const float* ad = ada_k ? ada_k + (size_t)l * 6 * d : nullptr;
     if (!dit) {
-      if (l < a.depth / 2) {
-        // skips are only ever GEMM A operands: keep them in the operand dtype
-        KCK(f32_to_op(bf, (const float*)h, (int64_t)rows * d, op(b.skips[l], ro, d), st));
+      const int half = a.depth / 2;
+      if (l < half) {
+        // skips.append(x) (unett.py:283-284): layer l reads xs[l] and writes xs[l+1], so xs[l] stays
+        // the skip connection without a copy
+        h_in = res(b.xs[l]);
+        h = res(b.xs[l + 1]);
+        KCK(rms_norm_g(bf, h_in, r16, rows, d, Ly.g_attn, aop, st));
       } else {
-        // skip_proj(cat(x, skip)) = x.W1^T + skip.W2^T (unett.py:288-297)
-        KCK(f32_to_op(bf, (const float*)h, (int64_t)rows * d, aop, st));
-        GemmArgs g = gargs(aop, d, Ly.skip1, rows, h2, d);
-        KCK(gemm(bf, EPI_STORE, g, st));
-        g = gargs(op(b.skips[a.depth - 1 - l], ro, d), d, Ly.skip2, rows, h2, d);
-        KCK(gemm(bf, EPI_RESID, g, st));
-        std::swap(h, h2);
+        // x = skip_proj(cat(x, skips.pop())) (unett.py:288-297): ONE GEMM over K = 2d whose A columns
+        // [d, 2d) come from the skip buffer; then attention/FFN update the result in place
+        void* x_prev = h;
+        h = res(b.pp[(l - half) & 1]);
+        h_in = nullptr;
+        GemmArgs g = gargs(x_prev, d, Ly.skip, rows, h, d);
+        g.A2 = res(b.xs[a.depth - 1 - l]);
+        g.k_split = d;
+        KCK(gemm(bf, r16 ? EPI_STORE16 : EPI_STORE, g, st));
+        KCK(rms_norm_g(bf, h, r16, rows, d, Ly.g_attn, aop, st));
       }
-      KCK(rms_norm_g(bf, (const float*)h, rows, d, Ly.g_attn, aop, st));
     } else {
-      KCK(ln_modulate(bf, h, r16, rows, d, ad /*shift_msa*/, ad + d /*scale_msa*/, aop, st));
+      if (do_ln) KCK(ln_modulate(bf, h, r16, rows, d, ad /*shift_msa*/, ad + d /*scale_msa*/, aop, st));
     }
     {
       GemmArgs g = gargs(aop, d, Ly.qkv, rows, nullptr, 0);
@@ -741,6 +794,7 @@ static int backbone_part(Ctx& c, int s0, int ns, hipStream_t st) {
     }
     {
       GemmArgs g = gargs(o, inner, Ly.out, rows, h, d);
+      g.resid = h_in;                      // UNetT first half: x_in + attn(.) -> the next buffer
       g.gate = ad ? ad + 2 * d : nullptr;  // gate_msa
       g.rowkeep = keep;                    // masked_fill of pad rows (modules.py:552-554)
       ProbeScope ps(e, KC_OUT, st, &c.site, &g.probe);
@@ -748,10 +802,11 @@ static int backbone_part(Ctx& c, int s0, int ns, hipStream_t st) {
     }
     {
       ProbeScope ps(e, KC_NORM, st, &c.site);
-      if (dit)
-        KCK(ln_modulate(bf, h, r16, rows, d, ad + 3 * d /*shift_mlp*/, ad + 4 * d /*scale_mlp*/, aop, st));
+      if (dit) {
+        if (do_ln) KCK(ln_modulate(bf, h, r16, rows, d, ad + 3 * d /*shift_mlp*/, ad + 4 * d /*scale_mlp*/, aop, st));
+      }
       else
-        KCK(rms_norm_g(bf, (const float*)h, rows, d, Ly.g_ff, aop, st));
+        KCK(rms_norm_g(bf, h, r16, rows, d, Ly.g_ff, aop, st));
     }
     {
       GemmArgs g = gargs(aop, d, Ly.ff1, rows, f, a.ff_dim);
@@ -769,7 +824,7 @@ static int backbone_part(Ctx& c, int s0, int ns, hipStream_t st) {
     const float* fin = ada_k + (size_t)a.depth * 6 * d;  // AdaLayerNorm_Final: (scale, shift)
     KCK(ln_modulate(bf, h, r16, rows, d, fin + d, fin, aop, st));
   } else {
-    KCK(rms_norm_g(bf, (const float*)h, rows, d, e->norm_out_g, aop, st));
+    KCK(rms_norm_g(bf, h, r16, rows, d, e->norm_out_g, aop, st));
   }
   GemmArgs g = gargs(aop, d, e->proj_out, rows, b.p + ro * a.mel_dim, a.mel_dim);
   KCK(gemm(bf, EPI_STORE, g, st));
@@ -814,11 +869,20 @@ extern "C" {
 const char* f5h_last_error(void) { return g_err.c_str(); }
 const char* f5h_version(void) { return "f5h 0.1 gfx950"; }
 
-int f5h_engine_create(const f5h_arch* arch, const f5h_weight* weights, int32_t n_weights, int32_t device,
-                      f5h_engine** out) {
+int f5h_engine_create_views(const f5h_arch* arch, const f5h_tensor_view* weights, int32_t n_weights, int32_t device,
+                            f5h_engine** out) {
   if (!out) return fail(F5H_EINVAL, "null out");
   *out = nullptr;
   RC(check_arch(arch));
+  if (n_weights < 0 || (n_weights > 0 && !weights)) return fail(F5H_EINVAL, "null weights");
+  for (int i = 0; i < n_weights; ++i) {
+    const f5h_tensor_view& v = weights[i];
+    if (!v.name || (!v.data && v.numel > 0) || v.numel < 0) return fail(F5H_EINVAL, "bad weight view");
+    if (v.dtype != F5H_DT_F32 && v.dtype != F5H_DT_BF16 && v.dtype != F5H_DT_F16)
+      return fail(F5H_EINVAL, std::string("weight ") + v.name + ": dtype must be F5H_DT_F32, _BF16 or _F16");
+    if (v.on_device != 0 && v.on_device != 1)
+      return fail(F5H_EINVAL, std::string("weight ") + v.name + ": on_device must be 0 or 1");
+  }
   HIPCK(hipSetDevice(device));
   f5h_engine* e = new f5h_engine();
   e->a = *arch;
@@ -828,9 +892,40 @@ int f5h_engine_create(const f5h_arch* arch, const f5h_weight* weights, int32_t n
   e->tdp = (arch->text_dim + 63) / 64 * 64;
   if (const char* gv = getenv("F5H_GRAPH")) e->graph_mode = atoi(gv) ? 1 : 0;
   if (const char* sv = getenv("F5H_SPLIT_CFG")) e->split_cfg = std::min(2, std::max(0, atoi(sv)));
+  // host views: staged once, in their own dtype, into temporaries freed after packing
   WMap W;
-  for (int i = 0; i < n_weights; ++i) W.m[weights[i].name] = {weights[i].data, weights[i].numel};
-  int rc = pack_all(e, W);
+  std::vector<void*> staged;
+  int rc = 0;
+  for (int i = 0; i < n_weights && !rc; ++i) {
+    const f5h_tensor_view& v = weights[i];
+    const size_t bytes = (size_t)v.numel * (v.dtype == F5H_DT_F32 ? 4 : 2);
+    const void* dp = v.data;
+    if (!v.on_device && bytes) {
+      void* t = nullptr;
+      if (hipMalloc(&t, bytes) != hipSuccess) {
+        rc = fail(F5H_EHIP, "weight staging allocation");
+        break;
+      }
+      staged.push_back(t);
+      if (hipMemcpy(t, v.data, bytes, hipMemcpyHostToDevice) != hipSuccess) {
+        rc = fail(F5H_EHIP, std::string("weight staging copy: ") + v.name);
+        break;
+      }
+      dp = t;
+    } else if (v.on_device && bytes) {
+      hipPointerAttribute_t at{};
+      if (hipPointerGetAttributes(&at, v.data) != hipSuccess || at.device != device) {
+        (void)hipGetLastError();
+        rc = fail(F5H_EINVAL, std::string("weight ") + v.name + ": on_device view is not memory of device " +
+                                  std::to_string(device));
+        break;
+      }
+    }
+    W.m[v.name] = WView{dp, v.dtype, v.numel};
+  }
+  if (!rc) rc = pack_all(e, W);
+  if (!rc && hipDeviceSynchronize() != hipSuccess) rc = fail(F5H_EHIP, "weight packing");
+  for (void* t : staged) (void)hipFree(t);
   if (rc) {
     f5h_engine_destroy(e);
     return rc;
@@ -853,9 +948,25 @@ int f5h_engine_create(const f5h_arch* arch, const f5h_weight* weights, int32_t n
   return 0;
 }
 
+int f5h_engine_create(const f5h_arch* arch, const f5h_weight* weights, int32_t n_weights, int32_t device,
+                      f5h_engine** out) {
+  if (n_weights < 0 || (n_weights > 0 && !weights)) return fail(F5H_EINVAL, "null weights");
+  std::vector<f5h_tensor_view> v((size_t)n_weights);
+  for (int i = 0; i < n_weights; ++i)
+    v[i] = f5h_tensor_view{weights[i].name, weights[i].data, F5H_DT_F32, 0, weights[i].numel};
+  return f5h_engine_create_views(arch, v.data(), n_weights, device, out);
+}
+
 void f5h_engine_destroy(f5h_engine* e) {
   if (!e) return;
+  if (!e->graphs.empty() || !e->graveyard.empty()) {
+    (void)hipSetDevice(e->dev);
+    (void)hipDeviceSynchronize();  // the engine is going away: no replay of its graphs may be in flight
+  }
   e->graphs.clear();
+  e->graveyard.clear();
+  for (hipEvent_t ev : e->ev_pool) (void)hipEventDestroy(ev);
+  e->ev_pool.clear();
   if (e->cap) (void)hipStreamDestroy(e->cap);
   if (e->cap2) (void)hipStreamDestroy(e->cap2);
   if (e->ev_fork) (void)hipEventDestroy(e->ev_fork);
@@ -887,18 +998,13 @@ static int check_ws(f5h_engine* e, int B, int N, int nfe, int use_cfg, void* w, 
 static int run_steps(Ctx& c, const f5h_sample_args* a, const void* ws);
 static int graph_get(Ctx& c, const GraphKey& key, bool split, const std::function<int(Ctx&)>& body,
                      std::shared_ptr<GraphEntry>& hold, int64_t replays);
+static int note_replays(f5h_engine* e, GraphEntry* g, hipStream_t st);
+static bool prologue_repeats(f5h_engine* e, const GraphKey& key);
 
 // The prologue as one captured graph per (workspace, shape): its ~56 launches otherwise cost more
 // host time than device time (profiles/r02_call_gaps_c2.txt). The inputs it reads are staged into
 // fixed workspace slots first, the grid is read from the device copy. F5H_PROLOGUE_GRAPH=0: eager.
-static int prologue_graph(Ctx& c, const f5h_sample_args* a, const void* ws) {
-  f5h_engine* e = c.e;
-  const size_t bn = (size_t)c.B * c.N;
-  HIPCK(hipMemcpyAsync(c.b.in_cond, a->cond, bn * e->a.mel_dim * sizeof(float), hipMemcpyDeviceToDevice, c.st));
-  HIPCK(hipMemcpyAsync(c.b.in_mask, a->cond_mask, bn, hipMemcpyDeviceToDevice, c.st));
-  if (c.nt > 0)
-    HIPCK(hipMemcpyAsync(c.b.in_text, a->text, (size_t)c.B * c.nt * sizeof(int64_t), hipMemcpyDeviceToDevice, c.st));
-  HIPCK(hipMemcpyAsync(c.b.in_dur, a->duration, (size_t)c.B * sizeof(int32_t), hipMemcpyDeviceToDevice, c.st));
+static GraphKey prologue_key(const Ctx& c, const void* ws) {
   GraphKey key{};
   key.ws = ws;
   key.kind = 1;
@@ -909,13 +1015,23 @@ static int prologue_graph(Ctx& c, const f5h_sample_args* a, const void* ws) {
   key.use_cfg = c.use_cfg;
   key.batch_mask = c.batch_mask;
   key.kernel_epoch = g_kernel_epoch.load();
+  return key;
+}
+static int prologue_graph(Ctx& c, const f5h_sample_args* a, const GraphKey& key) {
+  f5h_engine* e = c.e;
+  const size_t bn = (size_t)c.B * c.N;
+  HIPCK(hipMemcpyAsync(c.b.in_cond, a->cond, bn * e->a.mel_dim * sizeof(float), hipMemcpyDeviceToDevice, c.st));
+  HIPCK(hipMemcpyAsync(c.b.in_mask, a->cond_mask, bn, hipMemcpyDeviceToDevice, c.st));
+  if (c.nt > 0)
+    HIPCK(hipMemcpyAsync(c.b.in_text, a->text, (size_t)c.B * c.nt * sizeof(int64_t), hipMemcpyDeviceToDevice, c.st));
+  HIPCK(hipMemcpyAsync(c.b.in_dur, a->duration, (size_t)c.B * sizeof(int32_t), hipMemcpyDeviceToDevice, c.st));
   const Bufs& b = c.b;
   std::shared_ptr<GraphEntry> hold;
   RC(graph_get(c, key, false,
                [&](Ctx& cc) { return prologue(cc, nullptr, cc.nfe, b.in_cond, b.in_mask, b.in_text, b.in_dur); },
                hold, 1));
   HIPCK(hipGraphLaunch(hold->exec, c.st));
-  return 0;
+  return note_replays(e, hold.get(), c.st);
 }
 
 int f5h_sample(f5h_engine* e, void* stream, const f5h_sample_args* a, void* workspace, size_t workspace_bytes) {
@@ -944,8 +1060,9 @@ int f5h_sample(f5h_engine* e, void* stream, const f5h_sample_args* a, void* work
   }();
   HIPCK(grid_upload(a->t_grid, c.nfe + 1, c.b.tgrid, c.st));
   // the ODE evaluates fn at t_0 .. t_{nfe-1}
-  if (pro_graph && e->graph_mode && c.nt <= c.N)
-    RC(prologue_graph(c, a, workspace));
+  const GraphKey pkey = prologue_key(c, workspace);
+  if (pro_graph && e->graph_mode && c.nt <= c.N && prologue_repeats(e, pkey))
+    RC(prologue_graph(c, a, pkey));
   else
     RC(prologue(c, a->t_grid, c.nfe, a->cond, a->cond_mask, a->text, a->duration));
   const size_t ysz = (size_t)c.B * c.N * e->a.mel_dim;
@@ -1014,14 +1131,64 @@ static int run_steps(Ctx& c, const f5h_sample_args* a, const void* ws) {
   std::shared_ptr<GraphEntry> hold;  // keeps the replayed graph alive through the launch loop
   RC(graph_get(c, key, split, [&](Ctx& cc) { return enqueue_step(cc, a); }, hold, c.nfe));
   for (int k = 0; k < c.nfe; ++k) HIPCK(hipGraphLaunch(hold->exec, c.st));
+  return note_replays(e, hold.get(), c.st);
+}
+
+// Destroy graveyard entries that nothing replays any more: every event recorded after their
+// replays has completed and no caller holds them. Non-blocking (hipEventQuery); caller holds e->gm.
+static void reap_graphs(f5h_engine* e) {
+  auto done = [e](GraphEntry& g) {
+    size_t k = 0;
+    for (hipEvent_t ev : g.inflight) {
+      if (hipEventQuery(ev) == hipSuccess)
+        e->ev_pool.push_back(ev);
+      else
+        g.inflight[k++] = ev;
+    }
+    (void)hipGetLastError();  // hipErrorNotReady is the expected answer for a pending event
+    g.inflight.resize(k);
+    return k == 0;
+  };
+  for (auto& g : e->graphs)
+    if (g->inflight.size() > 4) done(*g);  // keep live entries' lists short
+  size_t k = 0;
+  for (size_t i = 0; i < e->graveyard.size(); ++i) {
+    auto& g = e->graveyard[i];
+    if (done(*g) && g.use_count() == 1) {
+      ++e->n_reaped;
+      continue;  // last reference: destroyed when the slot is overwritten or the vector shrinks
+    }
+    if (k != i) std::swap(e->graveyard[k], e->graveyard[i]);
+    ++k;
+  }
+  e->graveyard.resize(k);
+}
+
+// Record, on `st`, an event after the launches just enqueued from `g` (the entry stays in the
+// graveyard until it completes).
+static int note_replays(f5h_engine* e, GraphEntry* g, hipStream_t st) {
+  hipEvent_t ev = nullptr;
+  {
+    std::lock_guard<std::mutex> lk(e->gm);
+    if (!e->ev_pool.empty()) {
+      ev = e->ev_pool.back();
+      e->ev_pool.pop_back();
+    }
+  }
+  if (!ev) HIPCK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+  HIPCK(hipEventRecord(ev, st));
+  std::lock_guard<std::mutex> lk(e->gm);
+  g->inflight.push_back(ev);
   return 0;
 }
 
 // The cached graph for `key`, captured from `body` on the private capture stream(s) when absent.
+// An evicted entry moves to the graveyard (no device synchronisation, no wait under the mutex).
 static int graph_get(Ctx& c, const GraphKey& key, bool split, const std::function<int(Ctx&)>& body,
                      std::shared_ptr<GraphEntry>& hold, int64_t replays) {
   f5h_engine* e = c.e;
   std::lock_guard<std::mutex> g(e->gm);
+  reap_graphs(e);
   for (const auto& x : e->graphs)
     if (x->key == key) hold = x;
   if (!hold) {
@@ -1052,11 +1219,13 @@ static int graph_get(Ctx& c, const GraphKey& key, bool split, const std::functio
       ne->exec = nullptr;
       return fail(F5H_EHIP, std::string("hipGraphInstantiate: ") + hipGetErrorString(ie));
     }
-    if (e->graphs.size() >= 16) {  // evict the least recently used graph
+    if (e->graphs.size() >= kGraphCache) {  // evict the least recently used graph to the graveyard
       size_t lru = 0;
       for (size_t i = 1; i < e->graphs.size(); ++i)
         if (e->graphs[i]->stamp < e->graphs[lru]->stamp) lru = i;
-      e->graphs.erase(e->graphs.begin() + lru);  // destroyed now, or by its last replaying caller
+      e->graveyard.push_back(std::move(e->graphs[lru]));
+      e->graphs.erase(e->graphs.begin() + lru);
+      ++e->n_evicted;
     }
     e->graphs.push_back(ne);
     e->n_captures++;
@@ -1065,6 +1234,19 @@ static int graph_get(Ctx& c, const GraphKey& key, bool split, const std::functio
   hold->stamp = ++e->use_ctr;
   e->n_replays += replays;
   return 0;
+}
+
+// Prologue graphs pay off only when a shape repeats: true when the prologue graph for `key` is
+// cached or the key was seen before (remembered in a short FIFO); a first sighting is recorded.
+static bool prologue_repeats(f5h_engine* e, const GraphKey& key) {
+  std::lock_guard<std::mutex> g(e->gm);
+  for (const auto& x : e->graphs)
+    if (x->key == key) return true;
+  for (const auto& k : e->pro_seen)
+    if (k == key) return true;
+  if (e->pro_seen.size() >= 64) e->pro_seen.erase(e->pro_seen.begin());
+  e->pro_seen.push_back(key);
+  return false;
 }
 
 int f5h_forward(f5h_engine* e, void* stream, const f5h_forward_args* a, void* workspace, size_t workspace_bytes) {
@@ -1087,15 +1269,46 @@ int f5h_forward(f5h_engine* e, void* stream, const f5h_forward_args* a, void* wo
   c.L = e->a.backbone == F5H_DIT ? c.N : c.N + 1;
   c.batch_mask = a->use_batch_mask ? 1 : 0;
   if (e->a.backbone == F5H_DIT && a->N > 8192) return fail(F5H_EINVAL, "N exceeds the text position table (8192)");
+  if (a->text_cache < 0 || a->text_cache > 2) return fail(F5H_EINVAL, "text_cache must be 0, 1 or 2");
   RC(check_ws(e, c.B, c.N, 1, c.use_cfg, workspace, workspace_bytes, c));
-  float tg[2] = {a->t, a->t};
-  RC(prologue(c, tg, 1, a->cond, a->cond_mask, a->text, a->duration));
+  const bool cached = a->text_cache == 2;
+  if (a->t_dev) {  // time read on the stream: no host round trip (dit.py:332-333 takes a tensor)
+    HIPCK(hipMemcpyAsync(c.b.tgrid, a->t_dev, sizeof(float), hipMemcpyDeviceToDevice, c.st));
+    RC(prologue(c, nullptr, 1, a->cond, a->cond_mask, a->text, a->duration, cached));
+  } else {
+    float tg[2] = {a->t, a->t};
+    RC(prologue(c, tg, 1, a->cond, a->cond_mask, a->text, a->duration, cached));
+  }
   HIPCK(pack_y(e->bf, a->x, c.B * c.N, e->a.mel_dim, c.b.ypad, c.st));
   HIPCK(hipMemsetAsync(c.b.kstep, 0, sizeof(int), c.st));
-  c.site = 0;
-  RC(step_prep(c));
-  RC(backbone_step(c));
-  HIPCK(step_advance(c.b.kstep, e->ptick, c.st));
+  auto body = [](Ctx& cc) -> int {
+    cc.site = 0;
+    RC(step_prep(cc));
+    RC(backbone_step(cc));
+    KCK(step_advance(cc.b.kstep, cc.e->ptick, cc.st));
+    return 0;
+  };
+  if (e->graph_mode && a->text_cache != 0) {
+    // a kept workspace is reused call after call (the reference's ODE loop over the plugin): the
+    // backbone step (workspace buffers only) replays as one graph per (workspace, shape)
+    GraphKey key{};
+    key.ws = workspace;
+    key.kind = 2;
+    key.B = c.B;
+    key.N = c.N;
+    key.nt = c.nt;
+    key.nfe = 1;
+    key.use_cfg = c.use_cfg;
+    key.batch_mask = c.batch_mask;
+    key.probe = e->probe_class;
+    key.kernel_epoch = g_kernel_epoch.load();
+    std::shared_ptr<GraphEntry> hold;
+    RC(graph_get(c, key, false, body, hold, 1));
+    HIPCK(hipGraphLaunch(hold->exec, c.st));
+    RC(note_replays(e, hold.get(), c.st));
+  } else {
+    RC(body(c));
+  }
   HIPCK(copy_pred(c.b.p, c.S, c.L, e->a.backbone == F5H_DIT ? 0 : 1, e->a.mel_dim, e->a.mel_dim, a->pred, c.st));
   return 0;
 }

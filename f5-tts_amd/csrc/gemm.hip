@@ -82,6 +82,9 @@ hipError_t gemm(int compute, int epi, const GemmArgs& a, hipStream_t st) {
   // 8-column epilogue chunks: vector paths need 16 B alignment of every operand row
   if (epi == EPI_INPROJ && (a.ldc % 8 || a.ld_add % 8 || a.N % 8)) return hipErrorInvalidValue;
   if (epi == EPI_QKV && (a.N % 64)) return hipErrorInvalidValue;
+  // a second A panel starts on a stage boundary (64 bf16 / 32 fp32 columns)
+  if (a.A2 && (a.k_split <= 0 || a.k_split % 64 || a.k_split >= a.K)) return hipErrorInvalidValue;
+  if (a.resid && epi != EPI_RESID && epi != EPI_RESID16) return hipErrorInvalidValue;
   switch (compute) {
     case F5H_C_BF16: return hot_epi(epi) ? gemm_launch_bf16_a(epi, a, st) : gemm_launch_bf16_b(epi, a, st);
     case F5H_C_FP16: return hot_epi(epi) ? gemm_launch_f16_a(epi, a, st) : gemm_launch_f16_b(epi, a, st);

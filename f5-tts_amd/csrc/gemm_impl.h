@@ -178,11 +178,12 @@ F5H_DEV void epi8(const GemmArgs& g, int row, int col, V8 x, const V8* pre = nul
   if constexpr (EPI == EPI_RESID16) {
     // 16-bit residual stream: read, add in fp32 (same rounding as EPI_RESID), store rounded
     TC* C = reinterpret_cast<TC*>(g.C);
+    const TC* R = reinterpret_cast<const TC*>(g.resid ? g.resid : g.C);
     const float keep = (g.rowkeep && !g.rowkeep[row]) ? 0.f : 1.f;
     const bool v16 = full && (g.ldc % 8 == 0);
-    V8 c = v16 ? load8(C + off) : V8{};
+    V8 c = v16 ? load8(R + off) : V8{};
     if (!v16)
-      for (int e = 0; e < 8; ++e) c.v[e] = col + e < g.N ? to_f32(C[off + e]) : 0.f;
+      for (int e = 0; e < 8; ++e) c.v[e] = col + e < g.N ? to_f32(R[off + e]) : 0.f;
     V8 gt = g.gate ? (full ? load8(g.gate + col) : V8{}) : V8{{1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f}};
     if (g.gate && !full)
       for (int e = 0; e < 8; ++e) gt.v[e] = col + e < g.N ? g.gate[col + e] : 0.f;
@@ -195,11 +196,13 @@ F5H_DEV void epi8(const GemmArgs& g, int row, int col, V8 x, const V8* pre = nul
         if (col + e < g.N) C[off + e] = from_f32<TC>(x.v[e]);
     }
     return;
-  } else if constexpr (EPI == EPI_GELU_TANH || EPI == EPI_GELU_ERF_OP) {
+  } else if constexpr (EPI == EPI_GELU_TANH || EPI == EPI_GELU_ERF_OP || EPI == EPI_STORE16) {
+    if constexpr (EPI != EPI_STORE16) {
 #pragma unroll
-    for (int e = 0; e < 8; ++e)
-      x.v[e] = EPI == EPI_GELU_ERF_OP ? gelu_erf(x.v[e])
-                                      : (is16<TC>() ? gelu_tanh_fast(x.v[e]) : gelu_tanh(x.v[e]));
+      for (int e = 0; e < 8; ++e)
+        x.v[e] = EPI == EPI_GELU_ERF_OP ? gelu_erf(x.v[e])
+                                        : (is16<TC>() ? gelu_tanh_fast(x.v[e]) : gelu_tanh(x.v[e]));
+    }
     TC* C = reinterpret_cast<TC*>(g.C);
     if (full && g.ldc % 8 == 0) {
       store8<TC>(C + off, x);
@@ -218,9 +221,10 @@ F5H_DEV void epi8(const GemmArgs& g, int row, int col, V8 x, const V8* pre = nul
       for (int e = 0; e < 8; ++e) x.v[e] = gelu_erf(x.v[e]);
     } else if constexpr (EPI == EPI_RESID) {
       const float keep = (g.rowkeep && !g.rowkeep[row]) ? 0.f : 1.f;
-      V8 c = vec ? (pre ? *pre : load8(C + off)) : V8{};
+      const float* R = reinterpret_cast<const float*>(g.resid ? g.resid : g.C);
+      V8 c = vec ? (pre ? *pre : load8(R + off)) : V8{};
       if (!vec)
-        for (int e = 0; e < 8; ++e) c.v[e] = col + e < g.N ? C[off + e] : 0.f;
+        for (int e = 0; e < 8; ++e) c.v[e] = col + e < g.N ? R[off + e] : 0.f;
       V8 gt = g.gate ? (full ? load8(g.gate + col) : V8{}) : V8{{1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f}};
       if (g.gate && !full)
         for (int e = 0; e < 8; ++e) gt.v[e] = col + e < g.N ? g.gate[col + e] : 0.f;
@@ -313,12 +317,18 @@ __global__ __launch_bounds__(64 * WGM * WGN, 1) void gemm_kernel(GemmArgs g) {
     const int n = min(n0 + row, g.N - 1);  // likewise for weight rows past N
     boff[i] = (int64_t)n * g.ldw + swz(row, slot) * E;
   });
+  // A columns [k_split, K) come from the second panel A2 (cat(x, skip) of UNetT, unett.py:288-297):
+  // a stage never straddles k_split (a multiple of the stage width)
+  const TC* A2 = reinterpret_cast<const TC*>(g.A2);
   auto stage = [&](int buf, int k0) {
     uint4* As = lds + buf * stage_u4;
     uint4* Bs = As + BM * CPR;
+    const bool second = A2 && k0 >= g.k_split;
+    const TC* Ab = second ? A2 : A;
+    const int ka = second ? k0 - g.k_split : k0;
     static_for<0, AR>([&](auto I) {
       constexpr int i = decltype(I)::value;
-      __builtin_amdgcn_global_load_lds((const void*)(A + aoff[i] + k0), (LDS_PTR(void))(As + (i * NW + wid) * 64),
+      __builtin_amdgcn_global_load_lds((const void*)(Ab + aoff[i] + ka), (LDS_PTR(void))(As + (i * NW + wid) * 64),
                                        16, 0, 0);
     });
     static_for<0, BR>([&](auto I) {
@@ -357,7 +367,7 @@ __global__ __launch_bounds__(64 * WGM * WGN, 1) void gemm_kernel(GemmArgs g) {
                         MT * TPS * 8 <= 32;
   V8 pre[PREF ? MT : 1][PREF ? TPS : 1];
   if constexpr (PREF) {
-    const ResT<TC, EPI>* Cp = reinterpret_cast<const ResT<TC, EPI>*>(g.C);
+    const ResT<TC, EPI>* Cp = reinterpret_cast<const ResT<TC, EPI>*>(g.resid ? g.resid : g.C);
     const int fr_ = lane & 15, q_ = lane >> 4;
     (void)fr_;
     (void)q_;
@@ -493,7 +503,7 @@ __global__ __launch_bounds__(64 * WGM * WGN, 1) void gemm_kernel(GemmArgs g) {
             if constexpr (PREF) {
               ri[t].d = V8{};
             } else {
-              ri[t].d = ok ? load8(reinterpret_cast<const ResT<TC, EPI>*>(g.C) + (int64_t)row * g.ldc + col) : V8{};
+              ri[t].d = ok ? load8(reinterpret_cast<const ResT<TC, EPI>*>(g.resid ? g.resid : g.C) + (int64_t)row * g.ldc + col) : V8{};
             }
             if (ok && g.rowkeep && !g.rowkeep[row]) ri[t].keep = 0.f;
           } else {
@@ -562,6 +572,8 @@ __global__ __launch_bounds__(64 * WGM * WGN, 1) void gemm_kernel(GemmArgs g) {
               for (int e = 0; e < 8; ++e)
                 x.v[e] = EPI == EPI_GELU_ERF_OP ? gelu_erf(x.v[e])
                                                 : (is16<TC>() ? gelu_tanh_fast(x.v[e]) : gelu_tanh(x.v[e]));
+              store8<TC>(reinterpret_cast<TC*>(g.C) + (int64_t)row * g.ldc + col, x);
+            } else if constexpr (EPI == EPI_STORE16) {
               store8<TC>(reinterpret_cast<TC*>(g.C) + (int64_t)row * g.ldc + col, x);
             } else {  // EPI_STORE
               store8<float>(reinterpret_cast<float*>(g.C) + (int64_t)row * g.ldc + col, x);
@@ -665,6 +677,7 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(GemmArgs g) {
   constexpr int NI = NA > NB ? NA : NB;
   const int nI = grp == 0 ? NA : NB;
   const TC* src[NI];
+  const TC* src2[NI];  // A rows in the second A panel (g.A2: columns [k_split, K)), group 0 only
   uint32_t dst_off[NI];
 #pragma unroll
   for (int i = 0; i < NI; ++i) {
@@ -672,9 +685,11 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(GemmArgs g) {
     const int lc = swz64(row, lane & 3);  // logical chunk held at this physical slot
     if (grp == 0) {
       src[i] = A + (int64_t)min(m0 + row, g.M - 1) * g.lda + lc * 8;
+      src2[i] = g.A2 ? reinterpret_cast<const TC*>(g.A2) + (int64_t)min(m0 + row, g.M - 1) * g.lda + lc * 8 : src[i];
       dst_off[i] = (uint32_t)((i * 4 + w4) * 16 * 64);
     } else {
       src[i] = W + (int64_t)min(n0 + row, g.N - 1) * g.ldw + lc * 8;
+      src2[i] = src[i];
       dst_off[i] = (uint32_t)(BM * 64 + (i * 4 + w4) * 16 * 64);
     }
   }
@@ -684,10 +699,11 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(GemmArgs g) {
 #pragma unroll
     for (int s = 0; s < KS; ++s) {
       const int k0 = (p * KS + s) * 32;
+      const bool second = grp == 0 && g.A2 && k0 >= g.k_split;
 #pragma unroll
       for (int i = 0; i < NI; ++i)
         if (i < nI)
-          __builtin_amdgcn_global_load_lds((const void*)(src[i] + k0),
+          __builtin_amdgcn_global_load_lds((const void*)(second ? src2[i] + (k0 - g.k_split) : src[i] + k0),
                                            (LDS_PTR(void))(lds_c + slot * PB + s * SB + dst_off[i]), 16, 0, 0);
     }
   };
@@ -819,7 +835,7 @@ template <typename TC, int EPI, int BM, int BN, int WGM, int WGN, int NS, int KB
 static void launch_cfg(const GemmArgs& a, hipStream_t st) {
   const int tiles = ((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN);
   constexpr bool HOT = EPI == EPI_QKV || EPI == EPI_RESID || EPI == EPI_RESID16 || EPI == EPI_GELU_TANH ||
-                       EPI == EPI_GELU_ERF_OP || EPI == EPI_STORE;
+                       EPI == EPI_GELU_ERF_OP || EPI == EPI_STORE || EPI == EPI_STORE16;
   if constexpr (HOT) {
     if (a.N % BN == 0 && (EPI == EPI_QKV || a.ldc % 8 == 0)) {
       hipLaunchKernelGGL((gemm_kernel<TC, EPI, BM, BN, WGM, WGN, NS, true, KB>), dim3(tiles), dim3(64 * WGM * WGN), 0,
@@ -864,6 +880,7 @@ static hipError_t launch_epi(int epi, const GemmArgs& a, hipStream_t st) {
     case EPI_INPROJ: return launch_t<TC, EPI_INPROJ>(a, st);
     case EPI_QKV: return launch_t<TC, EPI_QKV>(a, st);
     case EPI_GELU_ERF_OP: return launch_t<TC, EPI_GELU_ERF_OP>(a, st);
+    case EPI_STORE16: return launch_t<TC, EPI_STORE16>(a, st);
   }
   return hipErrorInvalidValue;
 }

@@ -20,7 +20,10 @@ enum Epi {
   EPI_QKV = 7,        // RoPE + scatter to q/k/v [S,H,L,64]              (operand out)
   EPI_GELU_ERF_OP = 8,  // C = gelu_erf(acc + bias)                      (operand out; Vocos pwconv1)
   EPI_RESID16 = 9,   // C += gate[n] * (acc + bias) * rowkeep[m]        (operand dtype in/out: 16-bit residual)
+  EPI_STORE16 = 10,  // C = acc + bias                                   (operand out: UNetT skip_proj)
 };
+// EPI_RESID / EPI_RESID16 read the residual from `resid` when set (else from C) and write C, so a
+// layer can keep its input (UNetT skip connections) without a copy.
 
 // In-kernel launch probe (see probe_enter/probe_exit in common.h). Per launch site a row of
 // kProbeTicks x kProbeLanes entries, each on its own 128-B line (kProbeStride words): workgroup b
@@ -52,6 +55,8 @@ struct GemmArgs {
   void* q; void* k; void* v;
   float q_scale;                   // EPI_QKV: q is stored pre-multiplied by this (0 -> 1)
   DevProbe probe;                  // in-kernel launch timing (null slots: off)
+  const void* resid;               // EPI_RESID / EPI_RESID16 residual input (null: C)
+  const void* A2; int k_split;     // A columns [k_split, K) come from A2 (same lda), e.g. cat(x, skip)
 };
 
 // compute: ComputeMode (fp32 / bf16 / fp16 operands). A and W both in the operand dtype.
@@ -94,7 +99,8 @@ hipError_t silu_to_op(int compute, const float* x, void* y, int64_t n, hipStream
 hipError_t ln_modulate(int compute, const void* h, int h16, int M, int d, const float* shift, const float* scale,
                        void* out, hipStream_t st);
 // x_transformers RMSNorm: x / max(||x||, 1e-12) * sqrt(d) * g -> operand dtype
-hipError_t rms_norm_g(int compute, const float* h, int M, int d, const float* g, void* out, hipStream_t st);
+// h: fp32, or the operand dtype when h16 (16-bit residual stream)
+hipError_t rms_norm_g(int compute, const void* h, int h16, int M, int d, const float* g, void* out, hipStream_t st);
 hipError_t rope_table(int L, float2* out, hipStream_t st);
 // text tokens -> embeddings (dit.py:86-120 / unett.py:53-64), both branches
 struct TextEmbArgs {
@@ -153,7 +159,7 @@ hipError_t build_rowkeep(const int32_t* dur, int B, int S, int L, int off, uint8
 // kv_len[s] = dur[s % B] + off
 hipError_t build_kvlen(const int32_t* dur, int B, int S, int off, int32_t* kv, hipStream_t st);
 // h[s, 0, :] = temb (UNetT time token)
-hipError_t write_time_token(const float* temb, int S, int L, int d, float* h, hipStream_t st);
+hipError_t write_time_token(int compute, int h16, const float* temb, int S, int L, int d, void* h, hipStream_t st);
 // extract rows [s, 1..L-1] of pred -> dst [S, L-1, mel]
 hipError_t copy_pred(const float* p, int S, int L, int row_off, int mel, int64_t p_ld, float* dst, hipStream_t st);
 // Vocos decoder glue (vocos.hip)
@@ -167,5 +173,14 @@ hipError_t mel_mag(const float* spec, int64_t rows, int bins, int ld_spec, int l
 hipError_t mel_log(const float* mel, int B, int T, int n_mels, float* out, hipStream_t st);
 hipError_t f32_to_op(int compute, const float* x, int64_t n, void* out, hipStream_t st);
 hipError_t op_to_f32(int compute, const void* x, int64_t n, float* out, hipStream_t st);
+// Weight packing (engine creation): dst[i0*dst_st[0] + i1*dst_st[1] + i2*dst_st[2] + i3] =
+// cvt(src[i0*src_st[0] + i1*src_st[1] + i2*src_st[2] + i3*src_st[3]]) for i < n; element types
+// 0 = fp32, 1 = bf16, 2 = fp16 (f5h_dtype); conversions round to nearest even.
+struct PackArgs {
+  const void* src; int src_dt; int64_t src_st[4];
+  void* dst; int dst_dt; int64_t dst_st[3];
+  int n[4];
+};
+hipError_t pack_strided(const PackArgs& a, hipStream_t st);
 
 }  // namespace f5h

@@ -21,9 +21,11 @@ LIB_PATH = os.environ.get("F5H_LIB", os.path.join(_HERE, "lib", "libf5h.so"))
 F5H_DIT, F5H_UNETT = 0, 1
 F5H_FP32, F5H_BF16, F5H_FP16 = 0, 1, 2
 COMPUTE = {"fp32": F5H_FP32, "bf16": F5H_BF16, "fp16": F5H_FP16}
+F5H_DT_F32, F5H_DT_BF16, F5H_DT_F16 = 0, 1, 2
 
 # exported symbols, checked by tests/test_boundary.py against include/f5h.h
 EXPORTS = (
+    "f5h_engine_create_views",
     "f5h_engine_create",
     "f5h_engine_destroy",
     "f5h_workspace_size",
@@ -71,6 +73,11 @@ class Weight(ctypes.Structure):
     _fields_ = [("name", ctypes.c_char_p), ("data", ctypes.c_void_p), ("numel", ctypes.c_int64)]
 
 
+class TensorView(ctypes.Structure):
+    _fields_ = [("name", ctypes.c_char_p), ("data", ctypes.c_void_p), ("dtype", ctypes.c_int32),
+                ("on_device", ctypes.c_int32), ("numel", ctypes.c_int64)]
+
+
 class SampleArgs(ctypes.Structure):
     _fields_ = [
         ("B", ctypes.c_int32), ("N", ctypes.c_int32), ("nt", ctypes.c_int32), ("nfe", ctypes.c_int32),
@@ -88,6 +95,7 @@ class ForwardArgs(ctypes.Structure):
         ("text", ctypes.c_void_p), ("duration", ctypes.c_void_p), ("t", ctypes.c_float),
         ("use_batch_mask", ctypes.c_int32), ("pred", ctypes.c_void_p),
         ("cfg_infer", ctypes.c_int32), ("drop_audio_cond", ctypes.c_int32), ("drop_text", ctypes.c_int32),
+        ("t_dev", ctypes.c_void_p), ("text_cache", ctypes.c_int32),
     ]
 
 
@@ -110,6 +118,9 @@ def lib():
     vp, i32, i64, sz = ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64, ctypes.c_size_t
     L.f5h_engine_create.argtypes = [ctypes.POINTER(Arch), ctypes.POINTER(Weight), i32, i32, ctypes.POINTER(vp)]
     L.f5h_engine_create.restype = ctypes.c_int
+    L.f5h_engine_create_views.argtypes = [ctypes.POINTER(Arch), ctypes.POINTER(TensorView), i32, i32,
+                                          ctypes.POINTER(vp)]
+    L.f5h_engine_create_views.restype = ctypes.c_int
     L.f5h_engine_destroy.argtypes = [vp]
     L.f5h_engine_destroy.restype = None
     L.f5h_workspace_size.argtypes = [vp, i32, i32, i32, i32, i32]

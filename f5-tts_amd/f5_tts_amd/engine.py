@@ -12,6 +12,9 @@ import torch
 from . import _lib
 
 
+_VIEW_DT = {torch.float32: _lib.F5H_DT_F32, torch.bfloat16: _lib.F5H_DT_BF16, torch.float16: _lib.F5H_DT_F16}
+
+
 def _arch_struct(arch: dict, compute: str) -> _lib.Arch:
     a = _lib.Arch()
     a.backbone = _lib.F5H_DIT if arch["backbone"] == "DiT" else _lib.F5H_UNETT
@@ -46,23 +49,35 @@ class Engine:
         self.compute = compute
         self.device = torch.device("cuda", torch.cuda.current_device() if device is None else
                                    torch.device(device).index or 0)
-        host = {}
+        # typed views of the parameters in their own dtype and placement (utils_infer.py:190-232 leaves
+        # them fp16/bf16/fp32 on the device): the engine packs from them on the device, no host copy
+        keep, views = [], []
         for k, v in weights.items():
             k = k[len("transformer."):] if k.startswith("transformer.") else k
-            if isinstance(v, torch.Tensor):
-                v = v.detach().to("cpu", torch.float32).contiguous().numpy()
-            host[k] = np.ascontiguousarray(v, dtype=np.float32)
-        names = [k.encode() for k in host]
-        arr = (_lib.Weight * len(host))()
-        for i, (k, v) in enumerate(host.items()):
-            arr[i].name = names[i]
-            arr[i].data = v.ctypes.data
-            arr[i].numel = v.size
+            t = v.detach() if isinstance(v, torch.Tensor) else torch.from_numpy(np.ascontiguousarray(v))
+            if t.dtype not in _VIEW_DT:
+                t = t.to(torch.float32)
+            if t.is_cuda and t.device != self.device:
+                t = t.to(self.device)
+            t = t.contiguous()
+            keep.append(t)
+            views.append((k.encode(), t))
+        arr = (_lib.TensorView * len(views))()
+        for i, (name, t) in enumerate(views):
+            arr[i].name = name
+            arr[i].data = t.data_ptr()
+            arr[i].dtype = _VIEW_DT[t.dtype]
+            arr[i].on_device = int(t.is_cuda)
+            arr[i].numel = t.numel()
         a = _arch_struct(self.arch, compute)
         h = ctypes.c_void_p()
         with torch.cuda.device(self.device):
-            _lib.check(L.f5h_engine_create(ctypes.byref(a), arr, len(host), self.device.index, ctypes.byref(h)),
-                       "f5h_engine_create")
+            # device views are read on the engine's internal stream: the producers must be done
+            if any(t.is_cuda for t in keep):
+                torch.cuda.current_stream(self.device).synchronize()
+            _lib.check(L.f5h_engine_create_views(ctypes.byref(a), arr, len(views), self.device.index,
+                                                 ctypes.byref(h)), "f5h_engine_create_views")
+        del keep
         self._h = h
         self._lock = threading.Lock()
         # per-(stream, size) workspaces kept across calls: the engine's NFE-step hipGraph is keyed
@@ -152,11 +167,17 @@ class Engine:
                        "f5h_sample")
         return out, traj
 
-    def forward(self, x, cond, cond_mask, text, duration, t: float, use_batch_mask, cfg_infer=True,
-                drop_audio_cond=False, drop_text=False):
+    def forward_workspace(self, B, N, nt, cfg_infer=True):
+        """A workspace for `forward`; one kept across calls carries the text cache (text_cache=1/2)."""
+        return self._workspace(self.workspace_bytes(B, N, nt, 1, cfg_infer))
+
+    def forward(self, x, cond, cond_mask, text, duration, t, use_batch_mask, cfg_infer=True,
+                drop_audio_cond=False, drop_text=False, text_cache=0, workspace=None):
         """One backbone forward at time t (DiT.forward / UNetT.forward, dit.py:319-370).
         cfg_infer: packed cond/uncond -> pred [2B,N,mel]; else one branch -> [B,N,mel] honouring
-        drop_audio_cond / drop_text."""
+        drop_audio_cond / drop_text. t: a python float, or a one-element device tensor (read on the
+        stream, no host sync). text_cache: 0 = compute the text embedding for this call, 1 = compute
+        and keep it in `workspace`, 2 = reuse the one kept there (dit.py:294-317)."""
         B, N, mel = x.shape
         nt = text.shape[1]
         x = x.to(self.device, torch.float32).contiguous()
@@ -166,12 +187,20 @@ class Engine:
         dur = duration.to(self.device, torch.int32).contiguous()
         S = 2 * B if cfg_infer else B
         pred = torch.empty(S, N, mel, dtype=torch.float32, device=self.device)
-        ws = self._workspace(self.workspace_bytes(B, N, nt, 1, cfg_infer))
+        need = self.workspace_bytes(B, N, nt, 1, cfg_infer)
+        if text_cache and (workspace is None or workspace.numel() < need):
+            raise ValueError("text_cache needs a kept workspace of workspace_bytes(B, N, nt, 1, cfg_infer) bytes")
+        ws = workspace if workspace is not None and workspace.numel() >= need else self._workspace(need)
+        t_dev = None
+        if torch.is_tensor(t):
+            t_dev = t.reshape(-1)[:1].to(self.device, torch.float32).contiguous()
         a = _lib.ForwardArgs()
         a.B, a.N, a.nt = B, N, nt
         a.x, a.cond, a.cond_mask, a.text, a.duration = (x.data_ptr(), cond.data_ptr(), cmask.data_ptr(),
                                                         text.data_ptr(), dur.data_ptr())
-        a.t = float(t)
+        a.t = 0.0 if t_dev is not None else float(t)
+        a.t_dev = t_dev.data_ptr() if t_dev is not None else None
+        a.text_cache = int(text_cache)
         a.use_batch_mask = int(bool(use_batch_mask))
         a.pred = pred.data_ptr()
         a.cfg_infer = int(bool(cfg_infer))

@@ -4,8 +4,10 @@ Contract kept from the reference (SURVEY §1 "Public interface of L2"):
   * `__init__(**arch, text_num_embeds, mel_dim)`       utils_infer.py:258
   * `.dim`                                             cfm.py:67
   * `forward(x, cond, text, time, mask, drop_audio_cond, drop_text, cfg_infer, cache)`  dit.py:319-330
-  * `clear_cache()`                                    dit.py:316-317 (no-op: the engine keeps no
-    cross-call state, so the reference's thread-local text cache, dit.py:237-262, is not needed)
+  * `clear_cache()`                                    dit.py:316-317
+  * `forward(..., cache=True)` keeps the text embedding of the first call in a per-thread session
+    workspace (the reference's thread-local text_cond / text_uncond cache, dit.py:237-262, 294-317)
+    and reuses it until `clear_cache()`; the backbone step of a session replays as a hipGraph
 """
 
 from __future__ import annotations
@@ -54,6 +56,7 @@ class EngineBackbone(nn.Module):
         self.add_module("rotary_embed", rot)
         self.__dict__["_engines"] = {}
         self.__dict__["_engine_lock"] = threading.Lock()
+        self.__dict__["_tls"] = threading.local()
 
     # ------------------------------------------------------------------ engine cache
     def _weights_version(self):
@@ -96,16 +99,24 @@ class EngineBackbone(nn.Module):
         import copy
 
         for k, v in self.__dict__.items():
-            if k in ("_engines", "_engine_lock", "_mods"):
+            if k in ("_engines", "_engine_lock", "_mods", "_tls"):
                 continue
             new.__dict__[k] = copy.deepcopy(v, memo)
         new.__dict__.pop("_mods", None)
         new.__dict__["_engines"] = {}
         new.__dict__["_engine_lock"] = threading.Lock()
+        new.__dict__["_tls"] = threading.local()
         return new
 
+    def _sessions(self) -> dict:
+        tls = self.__dict__["_tls"]
+        if not hasattr(tls, "sessions"):
+            tls.sessions = {}
+        return tls.sessions
+
     def clear_cache(self):
-        pass
+        """Drop this thread's kept text embeddings (dit.py:316-317)."""
+        self._sessions().clear()
 
     # ------------------------------------------------------------------ plugin forward
     def forward(self, x, cond, text, time, mask=None, drop_audio_cond=False, drop_text=False, cfg_infer=False,
@@ -116,19 +127,32 @@ class EngineBackbone(nn.Module):
         cfg_infer=False: one branch (cfm.py:167-178) -> [B, N, mel], honouring drop_audio_cond and
         drop_text. `cond` is the already-masked step_cond; `time` a scalar or one value per sample
         (dit.py:332-333 repeats a scalar; distinct values run as groups of equal t, which is exact
-        because sequences of equal padded length N are independent in the backbone). `cache` has no
-        effect: the engine recomputes the text embedding per call (the reference's cache only avoids
-        recomputing it)."""
+        because sequences of equal padded length N are independent in the backbone). A scalar device
+        `time` is read on the stream (no host sync). `cache=True`: the first call of this thread's
+        session computes the text embedding (both branches) and keeps it, later calls reuse it until
+        clear_cache(), as dit.py:294-317 does; sessions are keyed by shape."""
         B, N = x.shape[:2]
         compute = compute or compute_for_dtype(next(self.parameters()).dtype)
         eng = self.get_engine(compute, x.device)
         dur = mask.sum(1) if mask is not None else torch.full((B,), N, device=x.device)
         ones = torch.ones(B, N, dtype=torch.uint8, device=x.device)
         use_mask = mask is not None
-        tv = time.reshape(-1).float().cpu() if torch.is_tensor(time) else torch.tensor([float(time)])
-        if tv.numel() not in (1, B):
-            raise ValueError(f"time must be a scalar or have one value per sample ({B}), got {tv.numel()}")
         flags = dict(cfg_infer=cfg_infer, drop_audio_cond=drop_audio_cond, drop_text=drop_text)
+        if not torch.is_tensor(time) or time.numel() == 1:
+            tval = time if torch.is_tensor(time) else float(time)
+            text_cache, ws = 0, None
+            if cache:
+                key = (compute, eng.device.index, B, N, text.shape[1], bool(cfg_infer), use_mask)
+                sess = self._sessions()
+                ws = sess.get(key)
+                text_cache = 2 if ws is not None else 1
+                if ws is None:
+                    ws = sess[key] = eng.forward_workspace(B, N, text.shape[1], cfg_infer)
+            pred = eng.forward(x, cond, ones, text, dur, tval, use_mask, text_cache=text_cache, workspace=ws, **flags)
+            return pred.to(x.dtype)
+        tv = time.reshape(-1).float().cpu()
+        if tv.numel() != B:
+            raise ValueError(f"time must be a scalar or have one value per sample ({B}), got {tv.numel()}")
         values = torch.unique(tv)
         if values.numel() == 1:
             pred = eng.forward(x, cond, ones, text, dur, float(values[0]), use_mask, **flags)

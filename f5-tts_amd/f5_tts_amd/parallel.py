@@ -52,17 +52,22 @@ def bucket(indices, frames, max_batch: int):
     return [idx[k:k + max_batch] for k in range(0, len(idx), max_batch)]
 
 
-def gather_mels(local: "dict[int, torch.Tensor]", device=None, group=None, layout=None):
+def gather_mels(local: "dict[int, torch.Tensor]", device=None, group=None, layout=None, num_channels=None):
     """All-gather finished mels {utt_index: [n_i, C]} from every rank.
     Returns {utt_index: tensor} with every utterance of the job (on every rank).
 
     layout: per rank, the [(utt_index, n_frames), ...] it holds, when every rank knows the plan
     (run_sharded does): then only the padded mel buffers travel and no count or index is read back
-    to the host, so the gather never waits for the device."""
+    to the host, so the gather never waits for the device. A rank may hold no utterance (fewer
+    utterances than ranks): its buffer is then all padding, on `device` (CPU when not given), with
+    `num_channels` channels (default: the local mels', else 100)."""
     world = dist.get_world_size(group)
     if layout is not None:
-        dev = device if device is not None else next(iter(local.values())).device
-        C = next(iter(local.values())).shape[-1] if local else 100
+        if device is not None:
+            dev = device
+        else:
+            dev = next(iter(local.values())).device if local else torch.device("cpu")
+        C = num_channels if num_channels is not None else (next(iter(local.values())).shape[-1] if local else 100)
         maxn = max(len(x) for x in layout)
         maxl = max((n for x in layout for _, n in x), default=0)
         buf = torch.zeros(maxn, maxl, C, dtype=torch.float32, device=dev)
@@ -72,7 +77,7 @@ def gather_mels(local: "dict[int, torch.Tensor]", device=None, group=None, layou
         dist.all_gather(bufs, buf, group=group)
         return {k: bufs[r][j, :n] for r in range(world) for j, (k, n) in enumerate(layout[r])}
     dev = device if device is not None else (next(iter(local.values())).device if local else torch.device("cpu"))
-    C = next(iter(local.values())).shape[-1] if local else 100
+    C = num_channels if num_channels is not None else (next(iter(local.values())).shape[-1] if local else 100)
     keys = sorted(local)
     cnt = torch.tensor([len(keys), max([local[k].shape[0] for k in keys], default=0)], dtype=torch.int64, device=dev)
     cnts = [torch.zeros_like(cnt) for _ in range(world)]
@@ -141,5 +146,5 @@ def run_sharded(utts, sample_fn, *, rank: int, world: int, max_batch: int = 32, 
     if world == 1:
         return local
     layout = [[(i, utts[i]["total"] - utts[i]["ref"]) for b in plan_all[r] for i in b] for r in range(world)]
-    return gather_mels(local, device=device, group=group, layout=layout)
+    return gather_mels(local, device=device, group=group, layout=layout, num_channels=utts[0]["cond"].shape[-1])
 

@@ -73,11 +73,30 @@ typedef struct f5h_weight {
   int64_t numel;
 } f5h_weight;
 
+/* Element type of a weight view. */
+enum f5h_dtype { F5H_DT_F32 = 0, F5H_DT_BF16 = 1, F5H_DT_F16 = 2 };
+
+/* One named parameter in its own dtype and placement: host memory, or device memory
+ * of the engine's device (e.g. a torch parameter's data_ptr() after model.to(dtype).to(device), as
+ * load_checkpoint leaves it, utils_infer.py:190-232). C-contiguous, state-dict name as f5h_weight. */
+typedef struct f5h_tensor_view {
+  const char* name;
+  const void* data;
+  int32_t dtype;             /* f5h_dtype */
+  int32_t on_device;         /* 0: host memory; 1: device memory of `device` */
+  int64_t numel;
+} f5h_tensor_view;
+
 typedef struct f5h_engine f5h_engine;
 
 /* Replaces: model construction + load_checkpoint (utils_infer.py:190-276): packs the
- * weights into the engine's device layout (bf16 or fp32 GEMM panels, conv taps, the
- * concatenated AdaLN matrix). Blocks until the upload is complete. */
+ * weights into the engine's device layout (bf16/fp16/fp32 GEMM panels, conv taps, the
+ * concatenated AdaLN matrix). Host views are staged to the device in their own dtype; every
+ * panel is packed on the device (no host fp32 copy of the model). Blocks until packing is complete;
+ * the views may be released afterwards. */
+int f5h_engine_create_views(const f5h_arch* arch, const f5h_tensor_view* weights, int32_t n_weights,
+                            int32_t device, f5h_engine** out);
+/* The same from fp32 host arrays (f5h_weight). */
 int f5h_engine_create(const f5h_arch* arch, const f5h_weight* weights, int32_t n_weights,
                       int32_t device, f5h_engine** out);
 void f5h_engine_destroy(f5h_engine* eng);
@@ -131,6 +150,14 @@ typedef struct f5h_forward_args {
   int32_t cfg_infer;
   int32_t drop_audio_cond;
   int32_t drop_text;
+  const float* t_dev;        /* DEVICE fp32 scalar time (read on the stream, no host sync), or NULL: use t */
+  /* The reference's text cache (dit.py:294-317: with cache=True the first forward of a sample()
+   * computes text_cond/text_uncond, later forwards reuse them until clear_cache()):
+   *   0: compute the text embedding (both branches) for this call only;
+   *   1: compute it and keep it in `workspace` for later calls;
+   *   2: reuse the one kept in `workspace` (same B, N, nt; the text and durations of the keeping call).
+   * With 1 or 2 the backbone step runs as a captured graph keyed by the workspace (graph mode). */
+  int32_t text_cache;
 } f5h_forward_args;
 int f5h_forward(f5h_engine* eng, void* stream, const f5h_forward_args* args, void* workspace,
                 size_t workspace_bytes);
@@ -150,8 +177,12 @@ int f5h_probe_read(f5h_engine* eng, int64_t* launches, double* total_ms);
  * first use and replays it nfe times; mode 0 launches the same sequence eagerly. The step touches
  * only workspace buffers, so the graph is keyed by (workspace, B, N, nfe, cfg, mask, probe,
  * kernel epoch); the caller's out/trajectory pointers are staged into the workspace per call.
- * Results are bitwise identical in both modes. f5h_graph_stats: captures so far, step replays so
- * far, graphs cached (LRU, at most 8; an evicted graph is destroyed only after its last user). */
+ * The call prologue (time/AdaLN tables, text embedding, hoisted input projection) is captured as
+ * a graph of its own only when its shape repeats (the first call of a shape runs it eagerly; env
+ * F5H_PROLOGUE_GRAPH=0: always eager). Results are bitwise identical in every mode.
+ * f5h_graph_stats: captures so far and graph replays so far (prologue and step graphs together),
+ * graphs cached (LRU of 16 over both kinds). An evicted graph is destroyed later, without any host
+ * wait, once the events recorded after its replays have completed and no caller holds it. */
 int f5h_set_graph_mode(f5h_engine* eng, int32_t mode);
 /* Launch chains of the captured step: 2 captures the conditional and the unconditional CFG branch as
  * two parallel chains (fork/join by events), so kernel boundaries of one branch overlap work of the

@@ -256,6 +256,11 @@ def main():
     jobs["e2_base_sample_b2"] = sample_job(e2, gc.E2B2, 2)
     jobs["base_batch_sample_b4"] = sample_job(base, gc.BASE_B4, 2)
     jobs["base_batch_sample_b4_masked"] = sample_job(base_masked, gc.BASE_B4, 2)
+    # round 3: the same three cases run by the reference in bf16 (same fp32 y0), i.e. the reference's
+    # own reduced-precision envelope for the C3 batch-mask path and the C5 (UNetT) path
+    jobs["e2_base_sample_b2_bf16"] = sample_job(e2, gc.E2B2, 2, dtype=torch.bfloat16)
+    jobs["base_batch_sample_b4_bf16"] = sample_job(base, gc.BASE_B4, 2, dtype=torch.bfloat16)
+    jobs["base_batch_sample_b4_masked_bf16"] = sample_job(base_masked, gc.BASE_B4, 2, dtype=torch.bfloat16)
     if not args.skip_c2:
         c2 = configs.get_arch("F5TTS_v1_Base")
         jobs["c2_sample_fp32"] = sample_job(c2, gc.C2, 16)

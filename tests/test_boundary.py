@@ -58,6 +58,8 @@ int main(void) {{
   printf("%zu %zu %zu %zu\\n", offsetof(f5h_sample_args, cfg_strength), offsetof(f5h_sample_args, out),
          offsetof(f5h_forward_args, t), offsetof(f5h_forward_args, pred));
   printf("%zu %zu\\n", sizeof(f5h_vocos_arch), offsetof(f5h_vocos_arch, compute));
+  printf("%zu %zu %zu %zu\\n", sizeof(f5h_tensor_view), offsetof(f5h_tensor_view, dtype),
+         offsetof(f5h_tensor_view, on_device), offsetof(f5h_tensor_view, numel));
   return 0;
 }}""")
     exe = tmp_path / "layout"
@@ -66,7 +68,9 @@ int main(void) {{
     want = [ctypes.sizeof(_lib.Arch), ctypes.sizeof(_lib.Weight), ctypes.sizeof(_lib.SampleArgs),
             ctypes.sizeof(_lib.ForwardArgs), _lib.SampleArgs.cfg_strength.offset, _lib.SampleArgs.out.offset,
             _lib.ForwardArgs.t.offset, _lib.ForwardArgs.pred.offset,
-            ctypes.sizeof(_lib.VocosArch), _lib.VocosArch.compute.offset]
+            ctypes.sizeof(_lib.VocosArch), _lib.VocosArch.compute.offset,
+            ctypes.sizeof(_lib.TensorView), _lib.TensorView.dtype.offset, _lib.TensorView.on_device.offset,
+            _lib.TensorView.numel.offset]
     assert [int(x) for x in got] == want
 
 
@@ -81,6 +85,18 @@ def test_errors_are_reported_not_crashing():
     h = ctypes.c_void_p()
     rc = L.f5h_engine_create(ctypes.byref(a), None, 0, 0, ctypes.byref(h))
     assert rc == -1 and b"multiple of 128" in L.f5h_last_error()
+    # typed views: a bad dtype or placement flag is rejected before any device work
+    good = _lib.Arch(backbone=0, dim=256, depth=1, heads=4, dim_head=64, ff_dim=512, text_dim=128,
+                     text_num_embeds=10, mel_dim=100, conv_layers=0, text_mask_padding=1, pe_attn_head=0,
+                     attn_mask_enabled=0, compute=1)
+    buf = (ctypes.c_float * 4)()
+    v = (_lib.TensorView * 1)()
+    v[0].name, v[0].data, v[0].dtype, v[0].on_device, v[0].numel = b"w", ctypes.addressof(buf), 7, 0, 4
+    rc = L.f5h_engine_create_views(ctypes.byref(good), v, 1, 0, ctypes.byref(h))
+    assert rc == -1 and b"dtype" in L.f5h_last_error()
+    v[0].dtype, v[0].on_device = _lib.F5H_DT_BF16, 3
+    rc = L.f5h_engine_create_views(ctypes.byref(good), v, 1, 0, ctypes.byref(h))
+    assert rc == -1 and b"on_device" in L.f5h_last_error()
     va = _lib.VocosArch(100, 500, 1536, 8, 1024, 256, 0)
     rc = L.f5h_vocos_create(ctypes.byref(va), None, 0, 0, ctypes.byref(h))
     assert rc == -1 and b"bad vocos arch" in L.f5h_last_error()

@@ -96,10 +96,10 @@ def _expected(u):
     return _fake_sample(cond, u["text"][None], torch.tensor([u["total"]]), torch.tensor([u["ref"]]))[0, u["ref"]:u["total"]]
 
 
-def _job_worker(rank, world, port, q):
+def _job_worker(rank, world, port, q, n=11):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    utts = _job()
+    utts = _job(n)
     calls = []
 
     def sample(cond, text, dur, lens):
@@ -130,6 +130,23 @@ def test_run_sharded_world2_gloo_every_utterance_once():
     assert all(ok for _, ok, _ in res), res
     assert sum(sum(c) for _, _, c in res) == 11
     assert all(max(c) <= 3 for _, _, c in res)
+    assert all(p.exitcode == 0 for p in procs)
+
+
+def test_run_sharded_world2_one_utterance_empty_rank():
+    """Fewer utterances than ranks: the rank holding none still joins the layout all-gather (CPU
+    device, channel count from the job) and ends with the one utterance."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_job_worker, args=(r, 2, port, q, 1)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+    assert all(ok for _, ok, _ in res), res
+    assert sorted(sum(c) for _, _, c in res) == [0, 1]
     assert all(p.exitcode == 0 for p in procs)
 
 
