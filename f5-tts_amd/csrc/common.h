@@ -113,12 +113,21 @@ F5H_DEV ProbeT probe_enter(const f5h::DevProbe& p) {
   }
   return r;
 }
+// timeline stamp `idx` of this workgroup (wave 0's view; only in the timeline launch)
+F5H_DEV void probe_mark(const f5h::DevProbe& p, const ProbeT& r, int idx) {
+  if (p.tl && r.k == 0 && threadIdx.x == 0) {
+    const int wg = blockIdx.x + gridDim.x * blockIdx.y;
+    if (wg < f5h::kTimelineWG) p.tl[wg * 4 + idx] = idx == 0 ? r.t0 : (unsigned long long)wall_clock64();
+  }
+}
 F5H_DEV void probe_exit(const f5h::DevProbe& p, const ProbeT& r) {
   if (p.slots && (threadIdx.x & 63) == 0 && r.k >= 0 && r.k < f5h::kProbeTicks && r.k % f5h::kProbeEvery == 0) {
     const int64_t i = probe_slot(r.k);
     atomicMax(p.slots + f5h::kProbeEnd + i, (unsigned long long)wall_clock64());
     if (threadIdx.x == 0) atomicMin(p.slots + i, r.t0);
   }
+  probe_mark(p, r, 0);
+  probe_mark(p, r, 3);
 }
 
 F5H_DEV float gelu_erf(float x) {  // nn.GELU(), modules.py:266 (explicit rounding, see gelu_tanh_fast)

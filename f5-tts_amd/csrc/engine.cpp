@@ -18,6 +18,8 @@
 #include <cstring>
 #include <algorithm>
 #include <atomic>
+#include <chrono>
+#include <cstdio>
 #include <memory>
 #include <functional>
 #include <mutex>
@@ -123,6 +125,7 @@ struct f5h_engine {
   int probe_class = -1;
   unsigned long long* pstamp = nullptr;
   unsigned long long* pslots = nullptr;
+  unsigned long long* ptl = nullptr;  // per-workgroup timeline of the first probed launch (kTimelineWG x 4)
   int* ptick = nullptr;
   double wall_khz = 0.0;
 };
@@ -531,11 +534,13 @@ struct ProbeScope {
   ProbeScope(f5h_engine* e_, int kc, hipStream_t s, int* site, DevProbe* kp = nullptr)
       : e(e_), st(s), on(e_->probe_class == kc && e_->pslots && *site < kProbeSites) {
     if (!on) return;
-    slots = e->pslots + (size_t)(*site)++ * kProbeRow;
+    const int s0 = (*site)++;
+    slots = e->pslots + (size_t)s0 * kProbeRow;
     if (kp) {
       self = true;
       kp->slots = slots;
       kp->tick = e->ptick;
+      kp->tl = s0 == 0 ? e->ptl : nullptr;  // the class's first launch site of a step, tick 0
     } else {
       (void)stamp_begin(slots, e->ptick, st);
     }
@@ -942,6 +947,13 @@ int f5h_engine_create_views(const f5h_arch* arch, const f5h_tensor_view* weights
     e->pstamp = reinterpret_cast<unsigned long long*>(p);
     e->pslots = e->pstamp + 64;
     e->ptick = reinterpret_cast<int*>(e->pstamp);
+    void* tl = nullptr;
+    if (hipMalloc(&tl, (size_t)kTimelineWG * 4 * sizeof(unsigned long long)) != hipSuccess) {
+      f5h_engine_destroy(e);
+      return fail(F5H_EHIP, "probe timeline buffer");
+    }
+    e->allocs.push_back(tl);
+    e->ptl = reinterpret_cast<unsigned long long*>(tl);
     if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, device) == hipSuccess) e->wall_khz = khz;
   }
   *out = e;
@@ -1134,6 +1146,18 @@ static int run_steps(Ctx& c, const f5h_sample_args* a, const void* ws) {
   return note_replays(e, hold.get(), c.st);
 }
 
+// F5H_HOST_TRACE=1: host time of the graph-cache phases on stderr (diagnostic)
+static bool host_trace() {
+  static const bool on = [] {
+    const char* v = getenv("F5H_HOST_TRACE");
+    return v && *v == '1';
+  }();
+  return on;
+}
+static double host_ms() {
+  return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
 // Destroy graveyard entries that nothing replays any more: every event recorded after their
 // replays has completed and no caller holds them. Non-blocking (hipEventQuery); caller holds e->gm.
 static void reap_graphs(f5h_engine* e) {
@@ -1187,8 +1211,15 @@ static int note_replays(f5h_engine* e, GraphEntry* g, hipStream_t st) {
 static int graph_get(Ctx& c, const GraphKey& key, bool split, const std::function<int(Ctx&)>& body,
                      std::shared_ptr<GraphEntry>& hold, int64_t replays) {
   f5h_engine* e = c.e;
+  const double t0 = host_trace() ? host_ms() : 0.0;
   std::lock_guard<std::mutex> g(e->gm);
+  const double t1 = host_trace() ? host_ms() : 0.0;
+  const int64_t reaped0 = e->n_reaped;
   reap_graphs(e);
+  const double t2 = host_trace() ? host_ms() : 0.0;
+  if (host_trace())
+    std::fprintf(stderr, "[f5h host] graph_get kind %d: lock %.3f ms, reap %.3f ms (%lld destroyed)\n", key.kind,
+                 t1 - t0, t2 - t1, (long long)(e->n_reaped - reaped0));
   for (const auto& x : e->graphs)
     if (x->key == key) hold = x;
   if (!hold) {
@@ -1203,6 +1234,7 @@ static int graph_get(Ctx& c, const GraphKey& key, bool split, const std::functio
     Ctx cc = c;
     cc.st = e->cap;
     cc.st2 = split ? e->cap2 : nullptr;
+    const double c0 = host_trace() ? host_ms() : 0.0;
     hipError_t be = hipStreamBeginCapture(e->cap, hipStreamCaptureModeThreadLocal);
     if (be != hipSuccess) return fail(F5H_EHIP, std::string("hipStreamBeginCapture: ") + hipGetErrorString(be));
     const int rc = body(cc);
@@ -1213,8 +1245,11 @@ static int graph_get(Ctx& c, const GraphKey& key, bool split, const std::functio
       if (rc) return rc;
       return fail(F5H_EHIP, std::string("hipStreamEndCapture: ") + hipGetErrorString(ce));
     }
+    const double c1 = host_trace() ? host_ms() : 0.0;
     const hipError_t ie = hipGraphInstantiate(&ne->exec, graph, nullptr, nullptr, 0);
     (void)hipGraphDestroy(graph);
+    if (host_trace())
+      std::fprintf(stderr, "[f5h host] capture %.3f ms, instantiate %.3f ms\n", c1 - c0, host_ms() - c1);
     if (ie != hipSuccess) {
       ne->exec = nullptr;
       return fail(F5H_EHIP, std::string("hipGraphInstantiate: ") + hipGetErrorString(ie));
@@ -1323,8 +1358,24 @@ int f5h_probe_enable(f5h_engine* e, int32_t kclass, int32_t enable) {
     HIPCK(hipMemset(e->pstamp, 0, 64 * sizeof(unsigned long long)));
     HIPCK(hipMemset(e->pslots, 0xff, (size_t)kProbeEnd * sizeof(unsigned long long)));
     HIPCK(hipMemset(e->pslots + kProbeEnd, 0, (size_t)kProbeEnd * sizeof(unsigned long long)));
+    HIPCK(hipMemset(e->ptl, 0, (size_t)kTimelineWG * 4 * sizeof(unsigned long long)));
     HIPCK(hipDeviceSynchronize());
   }
+  return 0;
+}
+
+int f5h_probe_timeline(f5h_engine* e, uint64_t* stamps, int32_t max_wg, int32_t* n_wg, double* tick_khz) {
+  if (!e || !stamps || max_wg <= 0) return fail(F5H_EINVAL, "null engine / buffer");
+  std::lock_guard<std::mutex> g(e->pm);
+  HIPCK(hipSetDevice(e->dev));
+  HIPCK(hipDeviceSynchronize());
+  const int n = std::min<int>(max_wg, kTimelineWG);
+  HIPCK(hipMemcpy(stamps, e->ptl, (size_t)n * 4 * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+  int last = 0;
+  for (int i = 0; i < n; ++i)
+    if (stamps[4 * i]) last = i + 1;
+  if (n_wg) *n_wg = last;
+  if (tick_khz) *tick_khz = e->wall_khz;
   return 0;
 }
 

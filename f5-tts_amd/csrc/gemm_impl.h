@@ -275,8 +275,13 @@ F5H_DEV void wait_stages(int n_stages) {
 
 // FAST: the launcher guarantees whole-column tiles (N % BN == 0, ldc % 8 == 0) for the hot
 // epilogues, so the epilogue is compiled without per-element column guards (see below).
+// Launch bounds: two 4-wave blocks per CU (2 waves per SIMD) must fit the register file, i.e. <= 256
+// VGPR+AGPR per lane. With a minimum of 1 wave per SIMD the compiler gave the 192x128 tile 116 VGPR
+// + 144 AGPR = 260: one block per CU, so the C2 QKV GEMM (480 tiles) ran as two rounds on 256 CUs
+// (tools/timeline_c2.py: second half of the grid entering 24 us after the first). Declaring 2 waves
+// per SIMD it fits in 212 VGPR, no spill.
 template <typename TC, int EPI, int BM, int BN, int WGM, int WGN, int NS, bool FAST = false, int KB = 128>
-__global__ __launch_bounds__(64 * WGM * WGN, 1) void gemm_kernel(GemmArgs g) {
+__global__ __launch_bounds__(64 * WGM * WGN, 2) void gemm_kernel(GemmArgs g) {
   const ProbeT probe_t = probe_enter(g.probe);
   typedef GemmCfg<BM, BN, WGM, WGN, NS, KB> C;
   constexpr int E = elems16<TC>();
@@ -389,6 +394,7 @@ __global__ __launch_bounds__(64 * WGM * WGN, 1) void gemm_kernel(GemmArgs g) {
     // the barrier then publishes every wave's part of it
     wait_stages<DPS>(min(NS - 2, nk - 1 - kt));
     __builtin_amdgcn_s_barrier();
+    if (kt == 0) probe_mark(g.probe, probe_t, 1);
     const uint32_t soff = (uint32_t)((kt % NS) * C::stage_bytes);
     u32x4 ar[SLABS][MT], br[SLABS][NT];
 #pragma unroll
@@ -447,6 +453,7 @@ __global__ __launch_bounds__(64 * WGM * WGN, 1) void gemm_kernel(GemmArgs g) {
     }
   }
   __syncthreads();
+  probe_mark(g.probe, probe_t, 2);
 
   // ---- epilogue, per wave and 16-row strip: accumulators -> the wave's LDS strip (fp32,
   // padded rows) -> 8-column chunks of whole rows, so the epilogue's global accesses are
@@ -756,6 +763,7 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(GemmArgs g) {
   for (int p = 0; p < D && p < nph; ++p) dma_phase(p);
   wait_dma(0, min(D, nph) - 1);
   __builtin_amdgcn_s_barrier();
+  probe_mark(g.probe, probe_t, 1);
   if (grp == 1) __builtin_amdgcn_s_barrier();  // group 1 sits out half-period 0
   for (int p = 0; p < nph; ++p) {
     // ---- mem(p): fragments of phase p, DMA of phase p+2, wait for own part of phase p+1
@@ -788,6 +796,7 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(GemmArgs g) {
   }
   if (grp == 0) __builtin_amdgcn_s_barrier();  // matches group 1's extra barrier
   __syncthreads();
+  probe_mark(g.probe, probe_t, 2);
 
   // ---- epilogue: as gemm_kernel, per wave and 16-row strip through LDS
   float* Cs = reinterpret_cast<float*>(lds) + wid * 16 * C::EPAD;

@@ -36,7 +36,11 @@ constexpr int64_t kProbeEnd = kProbeRow * kProbeSites;
 struct DevProbe {
   unsigned long long* slots;  // null: not probed
   const int* tick;            // device step tick
+  // per-workgroup timeline of the tick-0 launch of the first probed site (diagnostic, or null):
+  // tl[wg*4 + {0: entry, 1: main loop entered (first stage landed), 2: main loop done, 3: exit}]
+  unsigned long long* tl;
 };
+constexpr int kTimelineWG = 8192;  // workgroups recorded per timeline
 
 struct GemmArgs {
   const void* A; int64_t lda;      // [M,K] row-major, TA elements

@@ -33,6 +33,7 @@ EXPORTS = (
     "f5h_forward",
     "f5h_probe_enable",
     "f5h_probe_read",
+    "f5h_probe_timeline",
     "f5h_set_graph_mode",
     "f5h_set_cfg_streams",
     "f5h_graph_stats",
@@ -133,6 +134,9 @@ def lib():
     L.f5h_probe_enable.restype = ctypes.c_int
     L.f5h_probe_read.argtypes = [vp, ctypes.POINTER(i64), ctypes.POINTER(ctypes.c_double)]
     L.f5h_probe_read.restype = ctypes.c_int
+    L.f5h_probe_timeline.argtypes = [vp, ctypes.POINTER(ctypes.c_uint64), i32, ctypes.POINTER(i32),
+                                     ctypes.POINTER(ctypes.c_double)]
+    L.f5h_probe_timeline.restype = ctypes.c_int
     L.f5h_set_graph_mode.argtypes = [vp, i32]
     L.f5h_set_graph_mode.restype = ctypes.c_int
     L.f5h_set_cfg_streams.argtypes = [vp, i32]

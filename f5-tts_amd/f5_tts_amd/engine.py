@@ -219,6 +219,19 @@ class Engine:
         else:
             _lib.check(L.f5h_probe_enable(self._h, _lib.KCLASS[kclass], 1), "probe")
 
+    def probe_timeline(self, max_wg: int = 8192):
+        """Per-workgroup [entry, loop entered, loop done, exit] stamps (microseconds from the earliest
+        entry) of the probed class's first launch in the first probed step, as a [n_wg, 4] array."""
+        buf = (ctypes.c_uint64 * (4 * max_wg))()
+        n, khz = ctypes.c_int32(), ctypes.c_double()
+        _lib.check(_lib.lib().f5h_probe_timeline(self._h, buf, max_wg, ctypes.byref(n), ctypes.byref(khz)),
+                   "probe_timeline")
+        a = np.frombuffer(buf, dtype=np.uint64, count=4 * n.value).reshape(n.value, 4).astype(np.float64)
+        if n.value == 0 or khz.value <= 0:
+            return a
+        t0 = a[:, 0][a[:, 0] > 0].min()
+        return np.where(a > 0, (a - t0) * 1e3 / khz.value, np.nan)
+
     def probe_read(self):
         n = ctypes.c_int64()
         ms = ctypes.c_double()

@@ -170,6 +170,10 @@ int f5h_forward(f5h_engine* eng, void* stream, const f5h_forward_args* args, voi
  * 4 = conv, 5 = attention output-projection GEMM, 6 = pre-FFN norm (LayerNorm+modulate / RMSNorm). */
 int f5h_probe_enable(f5h_engine* eng, int32_t kclass, int32_t enable);
 int f5h_probe_read(f5h_engine* eng, int64_t* launches, double* total_ms);
+/* Per-workgroup timeline of the probed class's first launch in the first probed step (GEMM and
+ * attention kernels): stamps[4*w + {0 entry, 1 main loop entered, 2 main loop done, 3 exit}] in ticks of
+ * the device wall clock (tick_khz); n_wg = workgroups recorded (at most max_wg, at most 8192). */
+int f5h_probe_timeline(f5h_engine* eng, uint64_t* stamps, int32_t max_wg, int32_t* n_wg, double* tick_khz);
 
 /* NFE-step graph (the CFM.sample ODE loop, cfm.py:218 -> torchdiffeq Euler): with mode 1 (default;
  * env F5H_GRAPH=0 selects 0 at engine creation) f5h_sample captures one NFE step -- table-row

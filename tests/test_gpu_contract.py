@@ -51,7 +51,9 @@ def _plugin_euler(backbone, inp, duration, nfe, cfg, sway, y0, use_epss=True):
     cond = torch.nn.functional.pad(cond, (0, 0, 0, N - cond_len))
     step_cond = torch.where(cond_mask, cond, torch.zeros_like(cond))
     mask = lens_to_mask(duration) if B > 1 else None
-    t = time_grid(nfe, sway, use_epss, device=DEV, dtype=torch.float32)
+    # the grid in the parameter dtype, as cfm.py:211-216 builds it (then used in fp32 here)
+    pdtype = next(backbone.parameters()).dtype
+    t = time_grid(nfe, sway, use_epss, device="cpu", dtype=pdtype).float().to(DEV)
     y = y0.to(DEV)
     traj = [y]
     for k in range(nfe):
@@ -102,6 +104,35 @@ def test_plugin_packed_cfg_euler_loop_matches_reference():
     out, _ = _plugin_euler(m.transformer, inp, inp["duration"], nfe, cfg, sway, y0)
     torch.cuda.synchronize()
     assert gc.max_rel(out.cpu().numpy(), g["out"]) < FP32_TOL
+
+
+@pytest.mark.parametrize("pdtype", [torch.bfloat16, torch.float16])
+def test_typed_device_views_pack_like_host_fp32(pdtype):
+    """f5h_engine_create_views: an engine packed from the parameters where
+    load_checkpoint leaves them (bf16 / fp16 tensors on the device, utils_infer.py:190-232) is the
+    engine packed from fp32 host copies of the same values: identical forwards, bit for bit."""
+    _need_gpu()
+    from f5_tts_amd.engine import Engine
+
+    arch = gc.arch_of("tiny")
+    compute = "bf16" if pdtype == torch.bfloat16 else "fp16"
+    W = {k: v.to(pdtype) for k, v in synthetic.make_weights_torch(arch).items()}
+    dev_views = {k: v.to(DEV) for k, v in W.items()}
+    host_f32 = {k: v.float() for k, v in W.items()}  # exact: every 16-bit value is an fp32 value
+    e_dev = Engine(arch, dev_views, compute=compute, device=DEV)
+    e_host = Engine(arch, host_f32, compute=compute, device=DEV)
+    inp = synthetic.make_case(**gc.B3)
+    dur = torch.maximum(torch.maximum((inp["text"] != -1).sum(-1), inp["lens"]) + 1, inp["duration"])
+    N = int(dur.max())
+    x = synthetic.reference_noise(dur, 3).to(DEV)
+    cond = torch.nn.functional.pad(inp["cond"], (0, 0, 0, N - inp["cond"].shape[1])).to(DEV)
+    ones = torch.ones(3, N, dtype=torch.uint8, device=DEV)
+    args = (x, cond, ones, inp["text"].to(DEV), dur.to(DEV), 0.4, True)
+    a = e_dev.forward(*args)
+    b = e_host.forward(*args)
+    torch.cuda.synchronize()
+    assert torch.isfinite(a).all()
+    assert torch.equal(a, b)
 
 
 def test_plugin_text_cache_semantics():
@@ -173,7 +204,7 @@ def test_plugin_euler_loop_c2_time_close_to_engine_sample():
     print(f"C2 bf16: f5h_sample {t_eng * 1e3:.2f} ms, plugin Euler loop {t_plug * 1e3:.2f} ms "
           f"({t_plug / t_eng:.3f}x)")
     # same arithmetic up to the Euler update's rounding (torch fp32 vs the engine's cfg_euler)
-    assert gc.rel_err(o_plug.float().cpu().numpy(), o_eng.float().cpu().numpy()) < 1e-2
+    assert gc.rel_err(o_plug.float().cpu().numpy(), o_eng.float().cpu().numpy()) < 2e-3
     assert t_plug <= 1.1 * t_eng, (t_plug, t_eng)
 
 

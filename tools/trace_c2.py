@@ -16,7 +16,12 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [REPO, os.path.join(REPO, "f5-tts_amd")]
 
 
-def run(config="c2", calls=3):
+def run(config="c2", calls=None):
+    # F5H_TRACE_WARM / F5H_TRACE_CALLS (default 3 / 3): rocprofv3 of this ROCm build crashes after
+    # ~12-16k graph-launched dispatches (tools/probes/launch_cost count), ~2.6k per C2 call, so a
+    # graph-mode PMC pass uses 1 warm call + 2 marked calls
+    warm = int(os.environ.get("F5H_TRACE_WARM", "3"))
+    calls = int(os.environ.get("F5H_TRACE_CALLS", "3")) if calls is None else calls
     import torch
 
     import bench
@@ -33,7 +38,7 @@ def run(config="c2", calls=3):
     kw = dict(cond=inp["cond"].to(dev), text=inp["text"].to(dev), duration=inp["duration"],
               lens=inp["lens"], steps=case["nfe"], cfg_strength=case["cfg"],
               sway_sampling_coef=case["sway"], seed=0, keep_trajectory=False)
-    for _ in range(3):
+    for _ in range(warm):
         model.sample(**kw)
     torch.cuda.synchronize()
     marker = torch.rand(64, device=dev)
