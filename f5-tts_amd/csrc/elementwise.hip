@@ -2,25 +2,13 @@
 // 16-byte vector accesses). Each cites the reference op it restates.
 #include "common.h"
 #include "kernels.h"
+#include "lnrow.h"
 
 #include <algorithm>
 
 namespace f5h {
 
 static inline unsigned nblk(int64_t n, int t) { return (unsigned)((n + t - 1) / t); }
-
-template <typename T> F5H_DEV void store4(T* p, float a, float b, float c, float d);
-template <> F5H_DEV void store4<float>(float* p, float a, float b, float c, float d) {
-  *reinterpret_cast<float4*>(p) = make_float4(a, b, c, d);
-}
-template <> F5H_DEV void store4<bf16>(bf16* p, float a, float b, float c, float d) {
-  bf16x4 v = {f2bf(a), f2bf(b), f2bf(c), f2bf(d)};
-  *reinterpret_cast<bf16x4*>(p) = v;
-}
-template <> F5H_DEV void store4<f16>(f16* p, float a, float b, float c, float d) {
-  f16x4 v = {(f16)a, (f16)b, (f16)c, (f16)d};
-  *reinterpret_cast<f16x4*>(p) = v;
-}
 
 // ---------------------------------------------------------------- time embedding
 // SinusPositionEmbedding(256), scale 1000 (modules.py:157-169): [sin | cos](1000 t e^{-i ln1e4/127})
@@ -147,41 +135,10 @@ hipError_t silu_to_op(int compute, const float* x, void* y, int64_t n, hipStream
 // path uses (d = 256*NV), so every load is unconditional; d <= 2048, d % 4 == 0 otherwise.
 constexpr int MAXV = 8;  // float4 per lane
 
-// Row sum over the wave, the same value in every lane: DPP butterflies inside each 16-lane row
-// (xor 1, xor 2, half-mirror, mirror: VALU, no LDS round trip), then the four row sums by readlane.
-F5H_DEV float wave_sum_dpp(float v) {
-  auto dpp = [](float x, int ctrl) -> float {
-    switch (ctrl) {  // the control word must be an immediate
-      case 0xB1: return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0xB1, 0xF, 0xF, false));
-      case 0x4E: return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0x4E, 0xF, 0xF, false));
-      case 0x141: return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0x141, 0xF, 0xF, false));
-      default: return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0x140, 0xF, 0xF, false));
-    }
-  };
-  v += dpp(v, 0xB1);   // quad_perm [1,0,3,2]
-  v += dpp(v, 0x4E);   // quad_perm [2,3,0,1]
-  v += dpp(v, 0x141);  // row_half_mirror
-  v += dpp(v, 0x140);  // row_mirror: every lane of a row holds the row sum
-  const float r0 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 0));
-  const float r1 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 16));
-  const float r2 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 32));
-  const float r3 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 48));
-  return (r0 + r1) + (r2 + r3);
-}
-
 // LayerNorm(no affine, eps 1e-6) * (1 + scale) + shift (AdaLayerNorm modules.py:325, ff_norm :753,
-// AdaLayerNorm_Final :346). The modulation rows are loaded with the row, before the reductions.
-// TI: the residual stream's type (fp32, or the operand dtype on the 16-bit DiT path).
-template <typename TI> F5H_DEV float4 load4f(const TI* p);
-template <> F5H_DEV float4 load4f<float>(const float* p) { return *reinterpret_cast<const float4*>(p); }
-template <> F5H_DEV float4 load4f<bf16>(const bf16* p) {
-  const bf16x4 v = *reinterpret_cast<const bf16x4*>(p);
-  return make_float4((float)v[0], (float)v[1], (float)v[2], (float)v[3]);
-}
-template <> F5H_DEV float4 load4f<f16>(const f16* p) {
-  const f16x4 v = *reinterpret_cast<const f16x4*>(p);
-  return make_float4((float)v[0], (float)v[1], (float)v[2], (float)v[3]);
-}
+// AdaLayerNorm_Final :346), a wave per row (ln_mod_row, lnrow.h). The modulation rows are loaded with
+// the row, before the reductions. TI: the residual stream's type (fp32, or the operand dtype on the
+// 16-bit DiT path).
 template <typename TO, int NV, typename TI = float>
 __global__ __launch_bounds__(256) void ln_mod_kernel(const TI* h, int M, int d, const float* shift,
                                                      const float* scale, TO* out) {
@@ -202,28 +159,7 @@ __global__ __launch_bounds__(256) void ln_mod_kernel(const TI* h, int M, int d, 
     a[k] = ok ? sc[i] : make_float4(0, 0, 0, 0);
     b[k] = ok ? sh[i] : make_float4(0, 0, 0, 0);
   }
-  float s = 0.f;
-#pragma unroll
-  for (int k = 0; k < V; ++k) s += v[k].x + v[k].y + v[k].z + v[k].w;
-  const float mean = wave_sum_dpp(s) / d;
-  float q = 0.f;
-#pragma unroll
-  for (int k = 0; k < V; ++k) {
-    const int i = lane + 64 * k;
-    if (FIXED || i < n4) {
-      float p0 = v[k].x - mean, p1 = v[k].y - mean, p2 = v[k].z - mean, p3 = v[k].w - mean;
-      q += p0 * p0 + p1 * p1 + p2 * p2 + p3 * p3;
-    }
-  }
-  const float rstd = rsqrtf(wave_sum_dpp(q) / d + 1e-6f);
-#pragma unroll
-  for (int k = 0; k < V; ++k) {
-    const int i = lane + 64 * k;
-    if (FIXED || i < n4)
-      store4<TO>(out + (int64_t)row * d + 4 * i, (v[k].x - mean) * rstd * (1.f + a[k].x) + b[k].x,
-                 (v[k].y - mean) * rstd * (1.f + a[k].y) + b[k].y, (v[k].z - mean) * rstd * (1.f + a[k].z) + b[k].z,
-                 (v[k].w - mean) * rstd * (1.f + a[k].w) + b[k].w);
-  }
+  ln_mod_row<TO, V, FIXED>(v, a, b, lane, n4, d, out + (int64_t)row * d);
 }
 hipError_t ln_modulate(int compute, const void* hv, int h16, int M, int d, const float* shift, const float* scale,
                        void* out, hipStream_t st) {

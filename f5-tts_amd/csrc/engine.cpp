@@ -69,13 +69,13 @@ struct Layer {
 struct GraphKey {
   const void* ws;
   int kind;  // 0: one NFE step, 1: the call prologue (inputs staged into the workspace)
-  int B, N, nt, nfe, use_cfg, batch_mask, probe, split;
+  int B, N, nt, nfe, use_cfg, batch_mask, probe, split, lnf;
   uint64_t kernel_epoch;  // bumped whenever a forced GEMM config changes
   uint32_t cfg_bits;
   bool operator==(const GraphKey& o) const {
     return ws == o.ws && kind == o.kind && B == o.B && N == o.N && nt == o.nt && nfe == o.nfe && kernel_epoch == o.kernel_epoch &&
            use_cfg == o.use_cfg && batch_mask == o.batch_mask && probe == o.probe && cfg_bits == o.cfg_bits &&
-           split == o.split;
+           split == o.split && lnf == o.lnf;
   }
 };
 
@@ -113,6 +113,9 @@ struct f5h_engine {
   // at B = 1 the half-size launches cost more than the overlap gains, C2 +4 %), 1 = always, 0 = never
   // (env F5H_SPLIT_CFG, f5h_set_cfg_streams)
   int split_cfg = 2;
+  // residual GEMMs with fused LayerNorm tails on the 16-bit DiT path (env F5H_LN_FUSE=0 at creation,
+  // f5h_set_ln_fuse): 5 launches per block instead of 7, bitwise the same results
+  int ln_fuse = 1;
   uint64_t use_ctr = 0;
   int64_t n_captures = 0, n_replays = 0;
   // probe
@@ -434,6 +437,10 @@ struct WS {
   }
 };
 
+// arrival counters of the fused LayerNorm tails (GemmArgs::ln_cnt): one per 64-row block (the smallest
+// GEMM row tile) of each of the two CFG-chain parts
+static size_t lncnt_words(size_t rows) { return (2 * (rows / 64 + 2) + 3) / 4 * 4; }  // 16-B multiple (memset)
+
 struct Bufs {
   float *tsin, *th, *temb, *ada;
   void* tin_op;
@@ -448,6 +455,7 @@ struct Bufs {
   float2* rope;
   uint8_t* rowkeep;
   int32_t* kvlen;
+  uint32_t* lncnt;                    // fused LayerNorm tails: per-row-block arrival counters, two parts
   float *ada_cur, *temb_cur, *tgrid;  // the current step's table rows; device copy of the grid
   int* kstep;                         // device-side NFE step index
   float* y;                           // ODE state [B][N][mel] fp32
@@ -502,6 +510,7 @@ static void layout(const f5h_engine* e, WS& ws, Bufs& b, int B, int N, int nfe, 
   b.rope = ws.take<float2>((size_t)L * 32);
   b.rowkeep = ws.take<uint8_t>(rows);
   b.kvlen = ws.take<int32_t>(S);
+  b.lncnt = ws.take<uint32_t>(lncnt_words(rows));
   b.ada_cur = a.backbone == F5H_DIT ? ws.take<float>((size_t)e->ada.Npad) : nullptr;
   b.temb_cur = ws.take<float>((size_t)d);
   b.tgrid = ws.take<float>((size_t)nfe);
@@ -693,6 +702,11 @@ static int backbone_part(Ctx& c, int s0, int ns, hipStream_t st) {
     return v && *v == '1';
   }();
   const bool do_ln = !(skip_ln && r16);
+  // Fused LayerNorm tails (f5h_set_ln_fuse; off: separate ln_mod launches, same bits): on the 16-bit
+  // DiT path the out-projection and FFN2 GEMMs normalise and modulate their finished row blocks
+  // themselves, so a block runs 5 launches instead of 7 (gemm_impl.h ln_tail)
+  const bool ln_fuse = e->ln_fuse && do_ln && dit && r16 && (d == 512 || d == 768 || d == 1024);
+  uint32_t* lncnt = b.lncnt + (s0 ? lncnt_words((size_t)c.S * c.L) / 2 : 0);
   const size_t hsz = r16 ? es : sizeof(float);
   auto res = [&](void* base) -> void* { return (char*)base + ro * d * hsz; };
   void* bh = dit ? res(b.h) : res(b.xs[0]);
@@ -767,7 +781,9 @@ static int backbone_part(Ctx& c, int s0, int ns, hipStream_t st) {
         KCK(rms_norm_g(bf, h, r16, rows, d, Ly.g_attn, aop, st));
       }
     } else {
-      if (do_ln) KCK(ln_modulate(bf, h, r16, rows, d, ad /*shift_msa*/, ad + d /*scale_msa*/, aop, st));
+      // with fused tails only the first block's attention norm is a launch of its own
+      if (do_ln && !(ln_fuse && l > 0))
+        KCK(ln_modulate(bf, h, r16, rows, d, ad /*shift_msa*/, ad + d /*scale_msa*/, aop, st));
     }
     {
       GemmArgs g = gargs(aop, d, Ly.qkv, rows, nullptr, 0);
@@ -802,10 +818,16 @@ static int backbone_part(Ctx& c, int s0, int ns, hipStream_t st) {
       g.resid = h_in;                      // UNetT first half: x_in + attn(.) -> the next buffer
       g.gate = ad ? ad + 2 * d : nullptr;  // gate_msa
       g.rowkeep = keep;                    // masked_fill of pad rows (modules.py:552-554)
+      if (ln_fuse) {                       // + ff_norm of this block (modules.py:753)
+        g.ln_out = aop;
+        g.ln_shift = ad + 3 * d;           // shift_mlp
+        g.ln_scale = ad + 4 * d;           // scale_mlp
+        g.ln_cnt = lncnt;
+      }
       ProbeScope ps(e, KC_OUT, st, &c.site, &g.probe);
       KCK(gemm(bf, epi_resid, g, st));
     }
-    {
+    if (!ln_fuse) {
       ProbeScope ps(e, KC_NORM, st, &c.site);
       if (dit) {
         if (do_ln) KCK(ln_modulate(bf, h, r16, rows, d, ad + 3 * d /*shift_mlp*/, ad + 4 * d /*scale_mlp*/, aop, st));
@@ -821,13 +843,20 @@ static int backbone_part(Ctx& c, int s0, int ns, hipStream_t st) {
     {
       GemmArgs g = gargs(f, a.ff_dim, Ly.ff2, rows, h, d);
       g.gate = ad ? ad + 5 * d : nullptr;  // gate_mlp
+      if (ln_fuse) {  // + the next block's attn_norm (modules.py:325), or norm_out after the last (:346)
+        const float* nx = ada_k + (size_t)(l + 1) * 6 * d;
+        g.ln_out = aop;
+        g.ln_shift = l + 1 < a.depth ? nx : nx + d;  // AdaLayerNorm_Final rows are (scale, shift)
+        g.ln_scale = l + 1 < a.depth ? nx + d : nx;
+        g.ln_cnt = lncnt;
+      }
       ProbeScope ps(e, KC_FFN2, st, &c.site, &g.probe);
       KCK(gemm(bf, epi_resid, g, st));
     }
   }
   if (dit) {
     const float* fin = ada_k + (size_t)a.depth * 6 * d;  // AdaLayerNorm_Final: (scale, shift)
-    KCK(ln_modulate(bf, h, r16, rows, d, fin + d, fin, aop, st));
+    if (!ln_fuse) KCK(ln_modulate(bf, h, r16, rows, d, fin + d, fin, aop, st));
   } else {
     KCK(rms_norm_g(bf, h, r16, rows, d, e->norm_out_g, aop, st));
   }
@@ -897,6 +926,7 @@ int f5h_engine_create_views(const f5h_arch* arch, const f5h_tensor_view* weights
   e->tdp = (arch->text_dim + 63) / 64 * 64;
   if (const char* gv = getenv("F5H_GRAPH")) e->graph_mode = atoi(gv) ? 1 : 0;
   if (const char* sv = getenv("F5H_SPLIT_CFG")) e->split_cfg = std::min(2, std::max(0, atoi(sv)));
+  if (const char* lv = getenv("F5H_LN_FUSE")) e->ln_fuse = atoi(lv) != 0;
   // host views: staged once, in their own dtype, into temporaries freed after packing
   WMap W;
   std::vector<void*> staged;
@@ -1084,6 +1114,7 @@ int f5h_sample(f5h_engine* e, void* stream, const f5h_sample_args* a, void* work
   HIPCK(pack_y(e->bf, c.b.y, c.B * c.N, e->a.mel_dim, c.b.ypad, c.st));
   HIPCK(ptr_upload(a->trajectory, c.b.trajp, c.st));
   HIPCK(hipMemsetAsync(c.b.kstep, 0, sizeof(int), c.st));
+  HIPCK(hipMemsetAsync(c.b.lncnt, 0, lncnt_words((size_t)c.S * c.L) * sizeof(uint32_t), c.st));
   RC(run_steps(c, a, workspace));
   HIPCK(final_where_out(a->cond, a->cond_mask, c.b.y, a->out, c.B, c.N, e->a.mel_dim, c.st));
   return 0;
@@ -1138,6 +1169,7 @@ static int run_steps(Ctx& c, const f5h_sample_args* a, const void* ws) {
   key.probe = e->probe_class;
   const bool split = e->split_cfg == 1 || (e->split_cfg == 2 && c.B >= 4);
   key.split = split;
+  key.lnf = e->ln_fuse;
   key.kernel_epoch = g_kernel_epoch.load();
   std::memcpy(&key.cfg_bits, &a->cfg_strength, 4);
   std::shared_ptr<GraphEntry> hold;  // keeps the replayed graph alive through the launch loop
@@ -1316,6 +1348,7 @@ int f5h_forward(f5h_engine* e, void* stream, const f5h_forward_args* a, void* wo
   }
   HIPCK(pack_y(e->bf, a->x, c.B * c.N, e->a.mel_dim, c.b.ypad, c.st));
   HIPCK(hipMemsetAsync(c.b.kstep, 0, sizeof(int), c.st));
+  HIPCK(hipMemsetAsync(c.b.lncnt, 0, lncnt_words((size_t)c.S * c.L) * sizeof(uint32_t), c.st));
   auto body = [](Ctx& cc) -> int {
     cc.site = 0;
     RC(step_prep(cc));
@@ -1336,6 +1369,7 @@ int f5h_forward(f5h_engine* e, void* stream, const f5h_forward_args* a, void* wo
     key.use_cfg = c.use_cfg;
     key.batch_mask = c.batch_mask;
     key.probe = e->probe_class;
+    key.lnf = e->ln_fuse;
     key.kernel_epoch = g_kernel_epoch.load();
     std::shared_ptr<GraphEntry> hold;
     RC(graph_get(c, key, false, body, hold, 1));
@@ -1420,6 +1454,14 @@ int f5h_set_cfg_streams(f5h_engine* e, int32_t n) {
   if (n < 0 || n > 2) return fail(F5H_EINVAL, "cfg streams must be 0 (auto), 1 or 2");
   std::lock_guard<std::mutex> g(e->gm);
   e->split_cfg = n == 0 ? 2 : (n == 2 ? 1 : 0);
+  return 0;
+}
+
+int f5h_set_ln_fuse(f5h_engine* e, int32_t on) {
+  if (!e) return fail(F5H_EINVAL, "null engine");
+  if (on != 0 && on != 1) return fail(F5H_EINVAL, "ln fuse must be 0 or 1");
+  std::lock_guard<std::mutex> g(e->gm);
+  e->ln_fuse = on;
   return 0;
 }
 

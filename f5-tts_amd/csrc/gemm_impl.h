@@ -22,6 +22,7 @@
 #pragma once
 #include "common.h"
 #include "kernels.h"
+#include "lnrow.h"
 
 #include <cstdio>
 #include <cstdlib>
@@ -114,6 +115,81 @@ F5H_DEV V8 load8(const f16* p) {
   const f16x8 v = *reinterpret_cast<const f16x8*>(p);
   return V8{{(float)v[0], (float)v[1], (float)v[2], (float)v[3], (float)v[4], (float)v[5], (float)v[6], (float)v[7]}};
 }
+// 8 consecutive 16-bit values stored write-through (sc1: the line leaves this XCD's L2 for memory),
+// for bytes another workgroup of the same launch reads (cdna_hip_programming.md Guideline 16, R1).
+// base: the first byte the descriptor covers, bytes: its extent, off: byte offset of the 16 B.
+template <typename TC>
+F5H_DEV void store8_wt(const void* base, int bytes, int off, const V8& x) {
+  typedef unsigned u32v4 __attribute__((ext_vector_type(4)));
+  typedef typename Op16<TC>::v8 v8;
+  const v8 b = {from_f32<TC>(x.v[0]), from_f32<TC>(x.v[1]), from_f32<TC>(x.v[2]), from_f32<TC>(x.v[3]),
+                from_f32<TC>(x.v[4]), from_f32<TC>(x.v[5]), from_f32<TC>(x.v[6]), from_f32<TC>(x.v[7])};
+  const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, bytes, 0x00020000);
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32v4, b), r, off, 0, 16);
+}
+
+// Fused LayerNorm tail of a residual GEMM (GemmArgs::ln_cnt): rows [m0, m0 + BM) of C, complete
+// once every column tile of the row block has stored, are normalised and modulated into ln_out by
+// the block's last workgroup to finish; wave w takes rows m0 + w, m0 + w + NW, ... in batches of RB
+// (all of a batch's loads in flight before its reductions). Same row arithmetic as ln_mod_kernel.
+template <typename TC, int NV, int BM, int NW>
+F5H_DEV void ln_rows(const GemmArgs& g, int m0, int wid, int lane) {
+  constexpr int RPW = BM / NW, RB = RPW < 4 ? RPW : 4;
+  static_assert(RPW % RB == 0, "row batches");
+  const int d = g.N;
+  const float4* sh = reinterpret_cast<const float4*>(g.ln_shift);
+  const float4* sc = reinterpret_cast<const float4*>(g.ln_scale);
+  float4 a[NV], b[NV];
+#pragma unroll
+  for (int k = 0; k < NV; ++k) {
+    a[k] = sc[lane + 64 * k];
+    b[k] = sh[lane + 64 * k];
+  }
+  const TC* C = reinterpret_cast<const TC*>(g.C);
+  TC* out = reinterpret_cast<TC*>(g.ln_out);
+  for (int j0 = 0; j0 < RPW; j0 += RB) {
+    float4 v[RB][NV];
+#pragma unroll
+    for (int r = 0; r < RB; ++r) {
+      const int row = min(m0 + wid + NW * (j0 + r), g.M - 1);
+#pragma unroll
+      for (int k = 0; k < NV; ++k) v[r][k] = load4f<TC>(C + (int64_t)row * g.ldc + 4 * (lane + 64 * k));
+    }
+#pragma unroll
+    for (int r = 0; r < RB; ++r) {
+      const int row = m0 + wid + NW * (j0 + r);
+      if (row < g.M) ln_mod_row<TC, NV, true>(v[r], a, b, lane, 64 * NV, d, out + (int64_t)row * d);
+    }
+  }
+}
+
+template <typename TC, int BM, int NW>
+F5H_DEV void ln_tail(const GemmArgs& g, int m0, int ntn, int tid, uint4* lds) {
+  // every storing wave's write-through stores have completed before the workgroup arrives
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  int* flag = reinterpret_cast<int*>(lds);
+  if (tid == 0) {
+    uint32_t* cnt = g.ln_cnt + m0 / BM;
+    const uint32_t old = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int last = old == (uint32_t)(ntn - 1);
+    if (last) {
+      __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // zero for the next launch
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // drop this CU's stale L1 lines
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    *flag = last;
+  }
+  __syncthreads();
+  if (!*flag) return;
+  const int wid = tid >> 6, lane = tid & 63;
+  switch (g.N) {
+    case 1024: ln_rows<TC, 4, BM, NW>(g, m0, wid, lane); break;
+    case 768: ln_rows<TC, 3, BM, NW>(g, m0, wid, lane); break;
+    default: ln_rows<TC, 2, BM, NW>(g, m0, wid, lane); break;  // 512 (the launcher admits no other)
+  }
+}
+
 // the residual stream's element type: fp32, or the operand dtype for EPI_RESID16
 template <typename TC, int EPI>
 using ResT = typename std::conditional<EPI == EPI_RESID16, TC, float>::type;
@@ -573,7 +649,16 @@ __global__ __launch_bounds__(64 * WGM * WGN, 2) void gemm_kernel(GemmArgs g) {
               const V8& c = PREF ? pre[PREF ? i : 0][PREF ? t : 0] : ri.d;
 #pragma unroll
               for (int e = 0; e < 8; ++e) o.v[e] = resid_add(c.v[e], gate8.v[e], x.v[e], ri.keep);
-              store8<TC>(reinterpret_cast<TC*>(g.C) + (int64_t)row * g.ldc + col, o);
+              bool wt = false;
+              if constexpr (is16<TC>()) {
+                if (g.ln_cnt) {  // the row block's last workgroup reads these rows back (ln_tail)
+                  store8_wt<TC>(reinterpret_cast<const TC*>(g.C) + (int64_t)m0 * g.ldc,
+                                min(BM, g.M - m0) * (int)g.ldc * (int)sizeof(TC),
+                                ((row - m0) * (int)g.ldc + col) * (int)sizeof(TC), o);
+                  wt = true;
+                }
+              }
+              if (!wt) store8<TC>(reinterpret_cast<TC*>(g.C) + (int64_t)row * g.ldc + col, o);
             } else if constexpr (EPI == EPI_GELU_TANH || EPI == EPI_GELU_ERF_OP) {
 #pragma unroll
               for (int e = 0; e < 8; ++e)
@@ -592,6 +677,8 @@ __global__ __launch_bounds__(64 * WGM * WGN, 2) void gemm_kernel(GemmArgs g) {
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
       });
     }
+    if constexpr (EPI == EPI_RESID16 && is16<TC>())
+      if (g.ln_cnt) ln_tail<TC, BM, NW>(g, m0, ntn, tid, lds);
   }
   if constexpr (!FAST_EPI) {
 #pragma unroll
@@ -861,6 +948,20 @@ static hipError_t launch_t(const GemmArgs& a, hipStream_t st) {
   if (a.M == 0) return hipSuccess;
   int cfg = 0;
   if constexpr (is16<TC>()) cfg = gemm_select_cfg(a);
+  if (a.ln_cnt) {
+    // the fused LayerNorm tail runs in gemm_kernel's whole-column epilogue of EPI_RESID16 at d = 512,
+    // 768, 1024; any other case is the GEMM followed by the ln_modulate launch (same bits)
+    if (EPI != EPI_RESID16 || a.ldc != a.N || !is16<TC>()) return hipErrorInvalidValue;
+    const bool tail = cfg != 11 && a.N % 128 == 0 && (a.N == 512 || a.N == 768 || a.N == 1024);
+    if (!tail) {
+      GemmArgs b = a;
+      b.ln_cnt = nullptr;
+      const hipError_t err = launch_t<TC, EPI>(b, st);
+      if (err != hipSuccess) return err;
+      return ln_modulate(std::is_same<TC, bf16>::value ? F5H_C_BF16 : F5H_C_FP16, a.C, 1, a.M, a.N, a.ln_shift,
+                         a.ln_scale, a.ln_out, st);
+    }
+  }
   switch (cfg) {
     case 0: launch_cfg<TC, EPI, 64, 128, 2, 2, 3>(a, st); break;
     case 1: launch_cfg<TC, EPI, 128, 128, 2, 2, 2>(a, st); break;

@@ -61,6 +61,11 @@ struct GemmArgs {
   DevProbe probe;                  // in-kernel launch timing (null slots: off)
   const void* resid;               // EPI_RESID / EPI_RESID16 residual input (null: C)
   const void* A2; int k_split;     // A columns [k_split, K) come from A2 (same lda), e.g. cat(x, skip)
+  // EPI_RESID16 fused LayerNorm tail (ln_cnt set; ldc == N): the last tile of each row block to
+  // finish normalises and modulates the block's rows into ln_out ([M][N] operand dtype; the next
+  // sub-layer's AdaLN LayerNorm, ln_mod_row). ln_cnt: one zeroed arrival counter per row block,
+  // reset by its last arriver. Shapes the tail does not cover run as the GEMM + ln_modulate.
+  void* ln_out; const float* ln_shift; const float* ln_scale; uint32_t* ln_cnt;
 };
 
 // compute: ComputeMode (fp32 / bf16 / fp16 operands). A and W both in the operand dtype.
