@@ -71,10 +71,8 @@ F5H_DEV void attn_block(int& qb, int& bh) {
   bh = id / nqb;
 }
 
-// RS: K/V tiles staged through registers (global_load_dwordx4 issued one tile ahead of its
-// ds_write_b128, cdna_hip_programming.md T14) instead of LDS-DMA; the LDS image is the same.
-template <typename T, bool PRESCALED, int NW, bool RS>
-__global__ __launch_bounds__(64 * NW, 1) void attn16_kernel(AttnArgs a) {
+template <typename T, bool PRESCALED, int NW>
+__global__ __launch_bounds__(64 * NW, 8 / NW) void attn16_kernel(AttnArgs a) {
   typedef Op16<T> OP;
   typedef typename OP::v8 v8;
   typedef typename OP::v4 v4;
@@ -135,26 +133,6 @@ __global__ __launch_bounds__(64 * NW, 1) void attn16_kernel(AttnArgs a) {
       __builtin_amdgcn_global_load_lds((const void*)(V + off), (LDS_PTR(void))(Vs + (r * NW + wid) * 64), 16, 0, 0);
     }
   };
-  // register staging (RS): the same chunks into registers, written to the slot later
-  uint4 kst[CPW], vst[CPW];
-  auto gload = [&](int kt) {
-#pragma unroll
-    for (int r = 0; r < CPW; ++r) {
-      const int row = ((r * NW + wid) * 64 + lane) >> 3;
-      const int64_t off = (int64_t)min(kt * 64 + row, L - 1) * 64 + dsrc[r];
-      kst[r] = *reinterpret_cast<const uint4*>(K + off);
-      vst[r] = *reinterpret_cast<const uint4*>(V + off);
-    }
-  };
-  auto lwrite = [&](int buf) {
-    uint4* Ks = lds + buf * (TILE_B / 16);
-    uint4* Vs = Ks + 512;
-#pragma unroll
-    for (int r = 0; r < CPW; ++r) {
-      Ks[(r * NW + wid) * 64 + lane] = kst[r];
-      Vs[(r * NW + wid) * 64 + lane] = vst[r];
-    }
-  };
 
   const uint32_t lds0 = (uint32_t)(uintptr_t)(LDS_PTR(void))lds;
   uint32_t kaddr[4];
@@ -186,29 +164,15 @@ __global__ __launch_bounds__(64 * NW, 1) void attn16_kernel(AttnArgs a) {
     minit[r] = 0.f;
   }
 
-  if constexpr (RS) {
-    gload(0);
-    lwrite(0);
-    if (ntile > 1) {
-      gload(1);
-      lwrite(1);
-    }
-  } else {
-    dma(0, 0);
-    if (ntile > 1) dma(1, 1);
-  }
+  dma(0, 0);
+  if (ntile > 1) dma(1, 1);
   for (int kt = 0; kt < ntile; ++kt) {
     // tile kt landed for this wave's own DMA (tile kt+1 may stay in flight); the barrier
     // publishes every wave's part of it and retires all reads of slot (kt+2)%3 (= tile kt-1).
-    // RS: every ds_write of tile kt was issued an iteration earlier; lgkmcnt(0) retires them.
-    if constexpr (RS) {
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    } else {
-      if (kt + 1 < ntile)
-        asm volatile("s_waitcnt vmcnt(%0)" ::"i"(2 * CPW) : "memory");
-      else
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
+    if (kt + 1 < ntile)
+      asm volatile("s_waitcnt vmcnt(%0)" ::"i"(2 * CPW) : "memory");
+    else
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     if (kt == 0) probe_mark(a.probe, probe_t, 1);
     const uint32_t so = (uint32_t)((kt % NS) * TILE_B);
@@ -219,12 +183,7 @@ __global__ __launch_bounds__(64 * NW, 1) void attn16_kernel(AttnArgs a) {
       kf[0][ks] = lds_b128<0>(kaddr[ks] + so);
       kf[1][ks] = lds_b128<4096>(kaddr[ks] + so);
     });
-    if (kt + 2 < ntile) {
-      if constexpr (RS)
-        gload(kt + 2);  // registers now, LDS at the end of this iteration (T14 issue-early / write-late)
-      else
-        dma((kt + 2) % NS, kt + 2);
-    }
+    if (kt + 2 < ntile) dma((kt + 2) % NS, kt + 2);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 #pragma unroll
     for (int t = 0; t < 2; ++t)
@@ -341,10 +300,6 @@ __global__ __launch_bounds__(64 * NW, 1) void attn16_kernel(AttnArgs a) {
       __builtin_amdgcn_sched_barrier(0);
     });
     mma_chunk(std::integral_constant<int, 3>{});
-    // RS: slot (kt+2)%3 held tile kt-1, whose reads every wave finished before this iteration's
-    // barrier; the loads issued above have had the whole tile's compute to land
-    if constexpr (RS)
-      if (kt + 2 < ntile) lwrite((kt + 2) % NS);
   }
   probe_mark(a.probe, probe_t, 2);
   const float l_tot = lacc[0];
@@ -352,318 +307,6 @@ __global__ __launch_bounds__(64 * NW, 1) void attn16_kernel(AttnArgs a) {
   // Epilogue (T21): lane l < 32 holds columns 8k..8k+3 of its row, lane l + 32 columns 8k+4..8k+7; one
   // permlane32 swap per dword pairs groups k and k+1, so every lane stores 16 contiguous bytes
   // (lower lanes group k, upper lanes group k+1): 4 dwordx4 stores instead of 8 dwordx2
-  {
-    T* O = reinterpret_cast<T*>(a.o) + (((int64_t)s_idx * L + min(qrow, L - 1)) * a.H + head) * 64;
-#pragma unroll
-    for (int u = 0; u < 2; ++u)
-#pragma unroll
-      for (int r4 = 0; r4 < 4; r4 += 2) {
-        v4 w0 = {from_f32<T>(oacc[u][4 * r4 + 0] * inv), from_f32<T>(oacc[u][4 * r4 + 1] * inv),
-                 from_f32<T>(oacc[u][4 * r4 + 2] * inv), from_f32<T>(oacc[u][4 * r4 + 3] * inv)};
-        v4 w1 = {from_f32<T>(oacc[u][4 * r4 + 4] * inv), from_f32<T>(oacc[u][4 * r4 + 5] * inv),
-                 from_f32<T>(oacc[u][4 * r4 + 6] * inv), from_f32<T>(oacc[u][4 * r4 + 7] * inv)};
-        uint2 a2 = __builtin_bit_cast(uint2, w0), b2 = __builtin_bit_cast(uint2, w1);
-        auto sx = __builtin_amdgcn_permlane32_swap(a2.x, b2.x, false, false);
-        auto sy = __builtin_amdgcn_permlane32_swap(a2.y, b2.y, false, false);
-        const uint4 out = make_uint4(sx[0], sy[0], sx[1], sy[1]);
-        if (qrow < L) *reinterpret_cast<uint4*>(O + 32 * u + 8 * r4 + 8 * h) = out;
-      }
-  }
-  probe_exit(a.probe, probe_t);
-}
-
-// ---------------------------------------------------------------- two-tile software pipeline (T15)
-// The arithmetic of attn16_kernel (every O accumulator sees the same operands in the same order; the
-// lazy re-base decision for tile t+1 is taken after PV(t) was issued and before PV(t+1), as there)
-// except the row sums, which are fp32 VALU sums of the exp2 values (16 accumulator registers and 4
-// MFMAs per tile fewer), scheduled as a two-tile pipeline inside each wave
-// (cdna_hip_programming.md T15): iteration t issues QK^T(t+1) with the exp2/pack of P(t) in its MFMA
-// shadow, then PV(t) + row sums(t) with the max of S(t+1) in theirs, so a wave's VALU work issues
-// beside its own MFMAs instead of between them. K(t+1) and V(t) are read in iteration t; tiles are
-// staged by LDS-DMA two ahead into the 3-slot ring, as in attn16_kernel.
-template <typename T, bool PRESCALED, int NW>
-__global__ __launch_bounds__(64 * NW, 1) void attn16p_kernel(AttnArgs a) {
-  typedef Op16<T> OP;
-  typedef typename OP::v8 v8;
-  typedef typename OP::v4 v4;
-  const ProbeT probe_t = probe_enter(a.probe);
-  constexpr int TILE_B = 2 * 64 * 128;
-  constexpr int NS = 3;
-  constexpr int CPW = 512 / (64 * NW);
-  constexpr float THR = 8.f;
-  static_assert(CPW * 64 * NW == 512, "whole staging rounds");
-  __shared__ __attribute__((aligned(16))) uint4 lds[NS * TILE_B / 16];
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int h = lane >> 5;
-  int qb, bh;
-  attn_block(qb, bh);
-  const int s_idx = bh / a.H, head = bh - s_idx * a.H;
-  const int L = a.L;
-  const int64_t base = (int64_t)bh * L * 64;
-  const T* Q = reinterpret_cast<const T*>(a.q) + base;
-  const T* K = reinterpret_cast<const T*>(a.k) + base;
-  const T* V = reinterpret_cast<const T*>(a.v) + base;
-  int klen = L;
-  if (a.kv_len) klen = min(klen, a.kv_len[s_idx]);
-  const int ntile = (klen + 63) / 64;
-
-  const int qrow = qb * (32 * NW) + wid * 32 + (lane & 31);
-  v8 qf[4];
-#pragma unroll
-  for (int ks = 0; ks < 4; ++ks) {
-    uint4 v = *reinterpret_cast<const uint4*>(Q + (int64_t)min(qrow, L - 1) * 64 + ks * 16 + h * 8);
-    qf[ks] = __builtin_bit_cast(v8, v);
-    if constexpr (!PRESCALED) {
-      const float c = a.scale * 1.4426950408889634f;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) qf[ks][j] = from_f32<T>(to_f32(qf[ks][j]) * c);
-    }
-  }
-#pragma unroll
-  for (int ks = 0; ks < 4; ++ks) asm volatile("" ::"v"(qf[ks]));
-
-  int dsrc[CPW];
-#pragma unroll
-  for (int r = 0; r < CPW; ++r) {
-    const int p = (r * NW + wid) * 64 + lane, row = p >> 3, slot = p & 7;
-    dsrc[r] = swz128(row, slot) * 8;
-  }
-  auto dma = [&](int buf, int kt) {
-    uint4* Ks = lds + buf * (TILE_B / 16);
-    uint4* Vs = Ks + 512;
-#pragma unroll
-    for (int r = 0; r < CPW; ++r) {
-      const int row = ((r * NW + wid) * 64 + lane) >> 3;
-      const int64_t off = (int64_t)min(kt * 64 + row, L - 1) * 64 + dsrc[r];
-      __builtin_amdgcn_global_load_lds((const void*)(K + off), (LDS_PTR(void))(Ks + (r * NW + wid) * 64), 16, 0, 0);
-      __builtin_amdgcn_global_load_lds((const void*)(V + off), (LDS_PTR(void))(Vs + (r * NW + wid) * 64), 16, 0, 0);
-    }
-  };
-
-  const uint32_t lds0 = (uint32_t)(uintptr_t)(LDS_PTR(void))lds;
-  uint32_t kaddr[4];
-#pragma unroll
-  for (int ks = 0; ks < 4; ++ks) {
-    const int row = lane & 31;
-    kaddr[ks] = lds0 + row * 128 + swz128(row, ks * 2 + h) * 16;
-  }
-  const int G = lane >> 4, q4 = (lane & 15) >> 2, p4 = lane & 3;
-  uint32_t vaddr[2][2];
-#pragma unroll
-  for (int u = 0; u < 2; ++u)
-#pragma unroll
-    for (int g8 = 0; g8 < 2; ++g8) {
-      const int r1 = 4 * (G >> 1) + q4 + 8 * g8;
-      const int dh = 32 * u + 16 * (G & 1) + 4 * p4;
-      vaddr[u][g8] = lds0 + 64 * 128 + r1 * 128 + swz128(r1, dh >> 3) * 16 + ((dh >> 2) & 1) * 8;
-    }
-
-  float m_run = 0.f;
-  float lsum = 0.f;  // this lane's half of its query row's sum of P (fp32, on the VALU)
-  f32x16 oacc[2], minit;
-#pragma unroll
-  for (int r = 0; r < 16; ++r) {
-    oacc[0][r] = 0.f;
-    oacc[1][r] = 0.f;
-    minit[r] = 0.f;
-  }
-
-  // K fragments of the tile in slot `so` (8 ds_read_b128, hidden from hipcc's waitcnt bookkeeping)
-  u32x4 kf[2][4];
-  auto kread = [&](uint32_t so) {
-    static_for<0, 4>([&](auto KS) {
-      constexpr int ks = decltype(KS)::value;
-      kf[0][ks] = lds_b128<0>(kaddr[ks] + so);
-      kf[1][ks] = lds_b128<4096>(kaddr[ks] + so);
-    });
-  };
-  uint2 vf[2][2][2][2];
-  auto vread = [&](uint32_t so, auto U) {
-    constexpr int u = decltype(U)::value;
-    {
-      static_for<0, 2>([&](auto TT) {
-        constexpr int t = decltype(TT)::value;
-        static_for<0, 2>([&](auto S) {
-          constexpr int sx = decltype(S)::value;
-          vf[u][t][sx][0] = lds_tr_b64<(32 * t + 16 * sx) * 128>(vaddr[u][0] + so);
-          vf[u][t][sx][1] = lds_tr_b64<(32 * t + 16 * sx) * 128>(vaddr[u][1] + so);
-        });
-      });
-    }
-  };
-  auto fence_kf = [&]() {
-#pragma unroll
-    for (int t = 0; t < 2; ++t)
-#pragma unroll
-      for (int ks = 0; ks < 4; ++ks) asm volatile("" : "+v"(kf[t][ks]));
-  };
-  auto fence_vf = [&]() {
-#pragma unroll
-    for (int u = 0; u < 2; ++u)
-#pragma unroll
-      for (int t = 0; t < 2; ++t)
-#pragma unroll
-        for (int sx = 0; sx < 2; ++sx) {
-          asm volatile("" : "+v"(vf[u][t][sx][0]));
-          asm volatile("" : "+v"(vf[u][t][sx][1]));
-        }
-  };
-  // keys past klen in tile kt get p = 0
-  auto ragged = [&](f32x16 (&sc)[2], int kt) {
-    if (kt * 64 + 64 > klen) {
-      const int kbase = kt * 64 + 4 * h;
-#pragma unroll
-      for (int t = 0; t < 2; ++t)
-#pragma unroll
-        for (int r = 0; r < 16; ++r)
-          if (kbase + t * 32 + (r & 3) + 8 * (r >> 2) >= klen) sc[t][r] = -INFINITY;
-    }
-  };
-  auto rowmax = [&](const f32x16 (&sc)[2]) {
-    float mx = -INFINITY;
-#pragma unroll
-    for (int t = 0; t < 2; ++t)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) mx = fmaxf(mx, sc[t][r]);
-    return fmaxf(mx, xor32(mx));
-  };
-
-  // ---- prologue: tiles 0 and 1 staged, S(0) computed and based
-  dma(0, 0);
-  if (ntile > 1) dma(1, 1);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __builtin_amdgcn_s_barrier();
-  probe_mark(a.probe, probe_t, 1);
-  f32x16 sc[2];
-  kread(0);
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  fence_kf();
-  __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-  for (int t = 0; t < 2; ++t) {
-    sc[t] = OP::mma32(__builtin_bit_cast(v8, kf[t][0]), qf[0], minit);
-#pragma unroll
-    for (int ks = 1; ks < 4; ++ks) sc[t] = OP::mma32(__builtin_bit_cast(v8, kf[t][ks]), qf[ks], sc[t]);
-  }
-  ragged(sc, 0);
-  {
-    const float mx = rowmax(sc);
-    m_run = mx;  // first tile (>= 1 valid key): the running max starts at the tile max
-#pragma unroll
-    for (int t = 0; t < 2; ++t)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) sc[t][r] -= mx;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) minit[r] = -m_run;
-  }
-
-  // one pipelined iteration; MORE = a tile kt+1 exists (compile-time: the last tile is peeled, so no
-  // runtime branch lets the compiler hoist the exp2 work out of the MFMA shadow)
-  auto step = [&](int kt, auto MORE) {
-    constexpr bool more = decltype(MORE)::value;
-    if (kt > 0) {
-      // tile kt+1 (issued in iteration kt-1) landed for this wave's own DMA; the barrier publishes every
-      // wave's part of it and retires every read of slot (kt+2)%3 (tile kt-1: V read in iteration kt-1)
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_barrier();
-    }
-    if (kt + 2 < ntile) dma((kt + 2) % NS, kt + 2);
-    const uint32_t vso = (uint32_t)((kt % NS) * TILE_B);
-    if constexpr (more) kread((uint32_t)(((kt + 1) % NS) * TILE_B));
-    vread(vso, std::integral_constant<int, 0>{});
-    // ---- phase A: QK^T(kt+1) (8 MFMAs) with exp2 + pack + row sum of P(kt) in their shadow
-    v8 pf[2][2];
-    f32x16 sn[2];
-    auto exp_chunk = [&](auto C) {
-      constexpr int t = decltype(C)::value >> 1, sx = decltype(C)::value & 1;
-      float e[8];
-#pragma unroll
-      for (int j = 0; j < 8; ++j) e[j] = __builtin_amdgcn_exp2f(sc[t][8 * sx + j]);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) pf[t][sx][j] = from_f32<T>(e[j]);
-      lsum += ((e[0] + e[1]) + (e[2] + e[3])) + ((e[4] + e[5]) + (e[6] + e[7]));
-    };
-    if constexpr (more) {
-      asm volatile("s_waitcnt lgkmcnt(8)" ::: "memory");  // the 8 K reads (older than the 8 V reads)
-      fence_kf();
-    }
-    __builtin_amdgcn_sched_barrier(0);
-    static_for<0, 4>([&](auto C) {
-      constexpr int c = decltype(C)::value;
-      constexpr int t = c >> 1, k0 = (c & 1) * 2;
-      if constexpr (more) {
-        if constexpr (k0 == 0)
-          sn[t] = OP::mma32(__builtin_bit_cast(v8, kf[t][0]), qf[0], minit);
-        else
-          sn[t] = OP::mma32(__builtin_bit_cast(v8, kf[t][k0]), qf[k0], sn[t]);
-        sn[t] = OP::mma32(__builtin_bit_cast(v8, kf[t][k0 + 1]), qf[k0 + 1], sn[t]);
-      }
-      exp_chunk(C);
-      if constexpr (more) {
-        // per pair of MFMAs: 8 exp2 (TRANS), 4 packs and 8 adds
-        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-        __builtin_amdgcn_sched_group_barrier(0x400, 4, 0);
-        __builtin_amdgcn_sched_group_barrier(0x002, 6, 0);
-        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-        __builtin_amdgcn_sched_group_barrier(0x400, 4, 0);
-        __builtin_amdgcn_sched_group_barrier(0x002, 6, 0);
-      }
-      __builtin_amdgcn_sched_barrier(0);
-    });
-    // ---- phase B: PV(kt) (8 MFMAs: the V columns 0-31 first, 32-63 while their reads land) with the
-    // max of S(kt+1) in their shadow; per O accumulator the MFMA order is unchanged
-    vread(vso, std::integral_constant<int, 1>{});
-    asm volatile("s_waitcnt lgkmcnt(8)" ::: "memory");
-    fence_vf();
-    __builtin_amdgcn_sched_barrier(0);
-    auto pv = [&](auto U) {
-      constexpr int u = decltype(U)::value;
-      static_for<0, 4>([&](auto C) {
-        constexpr int t = decltype(C)::value >> 1, sx = decltype(C)::value & 1;
-        const uint4 w = make_uint4(vf[u][t][sx][0].x, vf[u][t][sx][0].y, vf[u][t][sx][1].x, vf[u][t][sx][1].y);
-        oacc[u] = OP::mma32(__builtin_bit_cast(v8, w), pf[t][sx], oacc[u]);
-      });
-    };
-    pv(std::integral_constant<int, 0>{});
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    fence_vf();
-    __builtin_amdgcn_sched_barrier(0);
-    pv(std::integral_constant<int, 1>{});
-    if constexpr (more) {
-      // the max of S(kt+1) between these 4 MFMAs
-      static_for<0, 4>([&](auto) {
-        __builtin_amdgcn_sched_group_barrier(0x008, 1, 1);
-        __builtin_amdgcn_sched_group_barrier(0x002, 5, 1);
-      });
-      ragged(sn, kt + 1);
-      const float mx = rowmax(sn);
-      if (!__all(mx <= THR)) {
-        // re-base the rows whose scores ran more than THR above m_run: O and l hold P(0..kt).V at the
-        // old base (PV(kt) issued above), S(kt+1) was computed against it
-        const float d = fmaxf(mx, 0.f);
-        const float alpha = __builtin_amdgcn_exp2f(-d);
-        m_run += d;
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          oacc[0][r] *= alpha;
-          oacc[1][r] *= alpha;
-          minit[r] = -m_run;
-        }
-        lsum *= alpha;
-#pragma unroll
-        for (int t = 0; t < 2; ++t)
-#pragma unroll
-          for (int r = 0; r < 16; ++r) sn[t][r] -= d;
-      }
-      sc[0] = sn[0];
-      sc[1] = sn[1];
-    }
-  };
-  for (int kt = 0; kt + 1 < ntile; ++kt) step(kt, std::true_type{});
-  step(ntile - 1, std::false_type{});
-  probe_mark(a.probe, probe_t, 2);
-  const float l_tot = lsum + xor32(lsum);  // the two half-waves hold the two key halves of a row
-  const float inv = l_tot > 0.f ? 1.f / l_tot : 0.f;
   {
     T* O = reinterpret_cast<T*>(a.o) + (((int64_t)s_idx * L + min(qrow, L - 1)) * a.H + head) * 64;
 #pragma unroll
@@ -747,48 +390,14 @@ __global__ __launch_bounds__(64) void attn_f32_kernel(AttnArgs a) {
   probe_exit(a.probe, probe_t);
 }
 
-// K/V staging: LDS-DMA (default) or register staging (T14; env F5H_ATTN_STAGE=reg). Measured at C2
-// (gpurun_out r03e, interleaved, one box): 37.5-37.6 us per launch with LDS-DMA against 39.0-39.1
-// with register staging, so the DMA form stays the default.
-static bool attn_reg_stage() {
-  static const bool rs = [] {
-    const char* v = getenv("F5H_ATTN_STAGE");
-    return v && !strcmp(v, "reg");
-  }();
-  return rs;
-}
-// F5H_ATTN_PIPE=1: the two-tile pipelined kernel (attn16p_kernel), A/B
-static bool attn_pipe() {
-  static const bool p = [] {
-    const char* v = getenv("F5H_ATTN_PIPE");
-    return v && *v == '1';
-  }();
-  return p;
-}
-
 template <typename T>
 static void launch16(const AttnArgs& a, hipStream_t st) {
-  constexpr int NW = 8;
+  constexpr int NW = 8;  // (two 4-wave workgroups per CU measured 40.3 vs 39.6 us at C2: kept one of 8)
   dim3 grid((a.L + 32 * NW - 1) / (32 * NW), a.S * a.H);
-  const bool rs = attn_reg_stage();
-  if (attn_pipe()) {
-    if (a.prescaled)
-      hipLaunchKernelGGL((attn16p_kernel<T, true, NW>), grid, dim3(64 * NW), 0, st, a);
-    else
-      hipLaunchKernelGGL((attn16p_kernel<T, false, NW>), grid, dim3(64 * NW), 0, st, a);
-    return;
-  }
-  if (a.prescaled) {
-    if (rs)
-      hipLaunchKernelGGL((attn16_kernel<T, true, NW, true>), grid, dim3(64 * NW), 0, st, a);
-    else
-      hipLaunchKernelGGL((attn16_kernel<T, true, NW, false>), grid, dim3(64 * NW), 0, st, a);
-  } else {
-    if (rs)
-      hipLaunchKernelGGL((attn16_kernel<T, false, NW, true>), grid, dim3(64 * NW), 0, st, a);
-    else
-      hipLaunchKernelGGL((attn16_kernel<T, false, NW, false>), grid, dim3(64 * NW), 0, st, a);
-  }
+  if (a.prescaled)
+    hipLaunchKernelGGL((attn16_kernel<T, true, NW>), grid, dim3(64 * NW), 0, st, a);
+  else
+    hipLaunchKernelGGL((attn16_kernel<T, false, NW>), grid, dim3(64 * NW), 0, st, a);
 }
 
 hipError_t attention(int compute, const AttnArgs& a, hipStream_t st) {

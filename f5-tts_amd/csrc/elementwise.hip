@@ -458,35 +458,61 @@ hipError_t pack_y(int compute, const float* y, int rows, int mel, void* ypad, hi
 // ---------------------------------------------------------------- CFG + Euler update
 // fn(t,x) = pred + (pred - null_pred) * cfg (cfm.py:190-191); torchdiffeq euler: y1 = y0 + dt * f
 template <typename TO>
-__global__ void cfg_euler_kernel(EulerArgs a, TO* ypad) {
+__global__ __launch_bounds__(256) void cfg_euler_kernel(EulerArgs a, TO* ypad) {
   int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int64_t total = (int64_t)a.B * a.N * a.mel;
-  if (i >= total) return;
-  const int c = (int)(i % a.mel);
-  const int64_t bn = i / a.mel;
-  const int b = (int)(bn / a.N), n = (int)(bn - (int64_t)b * a.N);
-  const float pc = a.p[(int64_t)b * a.p_seq_stride + (int64_t)(a.p_row_off + n) * a.p_ld + c];
-  float v = pc;
-  if (a.use_cfg) {
-    const float pu = a.p[(int64_t)(a.B + b) * a.p_seq_stride + (int64_t)(a.p_row_off + n) * a.p_ld + c];
-    v = add_nc(pc, mul_nc(sub_nc(pc, pu), a.cfg));
+  const int k = a.kstep ? *a.kstep : 0;  // read once: the last workgroup to arrive below bumps it
+  if (a.kstep && a.next_dst) {
+    // folded step bookkeeping (was a step_begin and a step_advance launch per NFE step): the next
+    // step's table row, then (below, after the update) the step-index bump
+    if (k + 1 < a.nfe) {
+      const float4* src = reinterpret_cast<const float4*>(a.next_src + (int64_t)(k + 1) * a.next_stride);
+      float4* dst = reinterpret_cast<float4*>(a.next_dst);
+      for (int64_t j = i; j < a.next_n / 4; j += (int64_t)gridDim.x * blockDim.x) dst[j] = src[j];
+    }
   }
   float dt = a.dt;
   float* traj = a.traj;
   if (a.kstep) {  // graph-replayable form: step index, grid and trajectory base live on the device
-    const int k = *a.kstep;
     dt = sub_nc(a.tgrid[k + 1], a.tgrid[k]);
     traj = a.trajp ? *a.trajp : nullptr;
     if (traj) traj += (int64_t)(k + 1) * total;
   }
-  const float y = add_nc(a.y[i], mul_nc(dt, v));
-  a.y[i] = y;
-  if (ypad) ypad[bn * 128 + c] = from_f32<TO>(y);
-  if (traj) traj[i] = y;
+  for (; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    const int c = (int)(i % a.mel);
+    const int64_t bn = i / a.mel;
+    const int b = (int)(bn / a.N), n = (int)(bn - (int64_t)b * a.N);
+    const float pc = a.p[(int64_t)b * a.p_seq_stride + (int64_t)(a.p_row_off + n) * a.p_ld + c];
+    float v = pc;
+    if (a.use_cfg) {
+      const float pu = a.p[(int64_t)(a.B + b) * a.p_seq_stride + (int64_t)(a.p_row_off + n) * a.p_ld + c];
+      v = add_nc(pc, mul_nc(sub_nc(pc, pu), a.cfg));
+    }
+    const float y = add_nc(a.y[i], mul_nc(dt, v));
+    a.y[i] = y;
+    if (ypad) ypad[bn * 128 + c] = from_f32<TO>(y);
+    if (traj) traj[i] = y;
+  }
+  if (a.kstep && a.arrive) {
+    // every thread of this workgroup has read k above: the last workgroup to arrive bumps the step
+    // index (and the probe tick) for the next step's launches
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      const unsigned old = __hip_atomic_fetch_add(a.arrive, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (old == gridDim.x - 1) {
+        *a.arrive = 0;
+        __hip_atomic_store(const_cast<int*>(a.kstep), k + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (a.tick) __hip_atomic_fetch_add(a.tick, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+  }
 }
 hipError_t cfg_euler(const EulerArgs& a, hipStream_t st) {
   const int64_t total = (int64_t)a.B * a.N * a.mel;
-  F5H_OP_DISPATCH(a.compute, T, hipLaunchKernelGGL(cfg_euler_kernel<T>, dim3(nblk(total, 256)), dim3(256), 0, st, a, (T*)a.ypad););
+  // at most 128 workgroups (a grid-stride loop covers the rest): the folded step-index bump costs one
+  // same-word atomic per workgroup, which serialise (~90 per us, MI355X_MICROARCH.md dequeue)
+  const unsigned blocks = std::min<unsigned>(128, std::max<unsigned>(1, nblk(total, 256)));
+  F5H_OP_DISPATCH(a.compute, T, hipLaunchKernelGGL(cfg_euler_kernel<T>, dim3(blocks), dim3(256), 0, st, a, (T*)a.ypad););
   return hipGetLastError();
 }
 

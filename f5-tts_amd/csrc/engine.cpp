@@ -69,13 +69,13 @@ struct Layer {
 struct GraphKey {
   const void* ws;
   int kind;  // 0: one NFE step, 1: the call prologue (inputs staged into the workspace)
-  int B, N, nt, nfe, use_cfg, batch_mask, probe, split, lnf;
+  int B, N, nt, nfe, use_cfg, batch_mask, probe, split;
   uint64_t kernel_epoch;  // bumped whenever a forced GEMM config changes
   uint32_t cfg_bits;
   bool operator==(const GraphKey& o) const {
     return ws == o.ws && kind == o.kind && B == o.B && N == o.N && nt == o.nt && nfe == o.nfe && kernel_epoch == o.kernel_epoch &&
            use_cfg == o.use_cfg && batch_mask == o.batch_mask && probe == o.probe && cfg_bits == o.cfg_bits &&
-           split == o.split && lnf == o.lnf;
+           split == o.split;
   }
 };
 
@@ -113,9 +113,6 @@ struct f5h_engine {
   // at B = 1 the half-size launches cost more than the overlap gains, C2 +4 %), 1 = always, 0 = never
   // (env F5H_SPLIT_CFG, f5h_set_cfg_streams)
   int split_cfg = 2;
-  // residual GEMMs with fused LayerNorm tails on the 16-bit DiT path (env F5H_LN_FUSE=0 at creation,
-  // f5h_set_ln_fuse): 5 launches per block instead of 7, bitwise the same results
-  int ln_fuse = 1;
   uint64_t use_ctr = 0;
   int64_t n_captures = 0, n_replays = 0;
   // probe
@@ -437,10 +434,6 @@ struct WS {
   }
 };
 
-// arrival counters of the fused LayerNorm tails (GemmArgs::ln_cnt): one per 64-row block (the smallest
-// GEMM row tile) of each of the two CFG-chain parts
-static size_t lncnt_words(size_t rows) { return (2 * (rows / 64 + 2) + 3) / 4 * 4; }  // 16-B multiple (memset)
-
 struct Bufs {
   float *tsin, *th, *temb, *ada;
   void* tin_op;
@@ -455,7 +448,6 @@ struct Bufs {
   float2* rope;
   uint8_t* rowkeep;
   int32_t* kvlen;
-  uint32_t* lncnt;                    // fused LayerNorm tails: per-row-block arrival counters, two parts
   float *ada_cur, *temb_cur, *tgrid;  // the current step's table rows; device copy of the grid
   int* kstep;                         // device-side NFE step index
   float* y;                           // ODE state [B][N][mel] fp32
@@ -510,7 +502,6 @@ static void layout(const f5h_engine* e, WS& ws, Bufs& b, int B, int N, int nfe, 
   b.rope = ws.take<float2>((size_t)L * 32);
   b.rowkeep = ws.take<uint8_t>(rows);
   b.kvlen = ws.take<int32_t>(S);
-  b.lncnt = ws.take<uint32_t>(lncnt_words(rows));
   b.ada_cur = a.backbone == F5H_DIT ? ws.take<float>((size_t)e->ada.Npad) : nullptr;
   b.temb_cur = ws.take<float>((size_t)d);
   b.tgrid = ws.take<float>((size_t)nfe);
@@ -661,6 +652,9 @@ static int prologue(Ctx& c, const float* t_host, int nt_vals, const float* cond,
   return 0;
 }
 
+// kstep buffer (64 ints): [0] the step index, [kArrive] the Euler launch's arrival counter
+constexpr int kArrive = 16;
+
 // Copy the step's table row (k = *kstep) to the fixed per-step buffer the layers read.
 static int step_prep(Ctx& c) {
   f5h_engine* e = c.e;
@@ -702,11 +696,6 @@ static int backbone_part(Ctx& c, int s0, int ns, hipStream_t st) {
     return v && *v == '1';
   }();
   const bool do_ln = !(skip_ln && r16);
-  // Fused LayerNorm tails (f5h_set_ln_fuse; off: separate ln_mod launches, same bits): on the 16-bit
-  // DiT path the out-projection and FFN2 GEMMs normalise and modulate their finished row blocks
-  // themselves, so a block runs 5 launches instead of 7 (gemm_impl.h ln_tail)
-  const bool ln_fuse = e->ln_fuse && do_ln && dit && r16 && (d == 512 || d == 768 || d == 1024);
-  uint32_t* lncnt = b.lncnt + (s0 ? lncnt_words((size_t)c.S * c.L) / 2 : 0);
   const size_t hsz = r16 ? es : sizeof(float);
   auto res = [&](void* base) -> void* { return (char*)base + ro * d * hsz; };
   void* bh = dit ? res(b.h) : res(b.xs[0]);
@@ -781,9 +770,7 @@ static int backbone_part(Ctx& c, int s0, int ns, hipStream_t st) {
         KCK(rms_norm_g(bf, h, r16, rows, d, Ly.g_attn, aop, st));
       }
     } else {
-      // with fused tails only the first block's attention norm is a launch of its own
-      if (do_ln && !(ln_fuse && l > 0))
-        KCK(ln_modulate(bf, h, r16, rows, d, ad /*shift_msa*/, ad + d /*scale_msa*/, aop, st));
+      if (do_ln) KCK(ln_modulate(bf, h, r16, rows, d, ad /*shift_msa*/, ad + d /*scale_msa*/, aop, st));
     }
     {
       GemmArgs g = gargs(aop, d, Ly.qkv, rows, nullptr, 0);
@@ -818,16 +805,10 @@ static int backbone_part(Ctx& c, int s0, int ns, hipStream_t st) {
       g.resid = h_in;                      // UNetT first half: x_in + attn(.) -> the next buffer
       g.gate = ad ? ad + 2 * d : nullptr;  // gate_msa
       g.rowkeep = keep;                    // masked_fill of pad rows (modules.py:552-554)
-      if (ln_fuse) {                       // + ff_norm of this block (modules.py:753)
-        g.ln_out = aop;
-        g.ln_shift = ad + 3 * d;           // shift_mlp
-        g.ln_scale = ad + 4 * d;           // scale_mlp
-        g.ln_cnt = lncnt;
-      }
       ProbeScope ps(e, KC_OUT, st, &c.site, &g.probe);
       KCK(gemm(bf, epi_resid, g, st));
     }
-    if (!ln_fuse) {
+    {
       ProbeScope ps(e, KC_NORM, st, &c.site);
       if (dit) {
         if (do_ln) KCK(ln_modulate(bf, h, r16, rows, d, ad + 3 * d /*shift_mlp*/, ad + 4 * d /*scale_mlp*/, aop, st));
@@ -843,20 +824,13 @@ static int backbone_part(Ctx& c, int s0, int ns, hipStream_t st) {
     {
       GemmArgs g = gargs(f, a.ff_dim, Ly.ff2, rows, h, d);
       g.gate = ad ? ad + 5 * d : nullptr;  // gate_mlp
-      if (ln_fuse) {  // + the next block's attn_norm (modules.py:325), or norm_out after the last (:346)
-        const float* nx = ada_k + (size_t)(l + 1) * 6 * d;
-        g.ln_out = aop;
-        g.ln_shift = l + 1 < a.depth ? nx : nx + d;  // AdaLayerNorm_Final rows are (scale, shift)
-        g.ln_scale = l + 1 < a.depth ? nx + d : nx;
-        g.ln_cnt = lncnt;
-      }
       ProbeScope ps(e, KC_FFN2, st, &c.site, &g.probe);
       KCK(gemm(bf, epi_resid, g, st));
     }
   }
   if (dit) {
     const float* fin = ada_k + (size_t)a.depth * 6 * d;  // AdaLayerNorm_Final: (scale, shift)
-    if (!ln_fuse) KCK(ln_modulate(bf, h, r16, rows, d, fin + d, fin, aop, st));
+    KCK(ln_modulate(bf, h, r16, rows, d, fin + d, fin, aop, st));
   } else {
     KCK(rms_norm_g(bf, h, r16, rows, d, e->norm_out_g, aop, st));
   }
@@ -926,7 +900,6 @@ int f5h_engine_create_views(const f5h_arch* arch, const f5h_tensor_view* weights
   e->tdp = (arch->text_dim + 63) / 64 * 64;
   if (const char* gv = getenv("F5H_GRAPH")) e->graph_mode = atoi(gv) ? 1 : 0;
   if (const char* sv = getenv("F5H_SPLIT_CFG")) e->split_cfg = std::min(2, std::max(0, atoi(sv)));
-  if (const char* lv = getenv("F5H_LN_FUSE")) e->ln_fuse = atoi(lv) != 0;
   // host views: staged once, in their own dtype, into temporaries freed after packing
   WMap W;
   std::vector<void*> staged;
@@ -1113,20 +1086,22 @@ int f5h_sample(f5h_engine* e, void* stream, const f5h_sample_args* a, void* work
     HIPCK(hipMemcpyAsync(a->trajectory, a->y0, ysz * sizeof(float), hipMemcpyDeviceToDevice, c.st));
   HIPCK(pack_y(e->bf, c.b.y, c.B * c.N, e->a.mel_dim, c.b.ypad, c.st));
   HIPCK(ptr_upload(a->trajectory, c.b.trajp, c.st));
-  HIPCK(hipMemsetAsync(c.b.kstep, 0, sizeof(int), c.st));
-  HIPCK(hipMemsetAsync(c.b.lncnt, 0, lncnt_words((size_t)c.S * c.L) * sizeof(uint32_t), c.st));
+  // step index and the Euler launch's arrival counter (kstep[kArrive]) start at 0; step 0's table row
+  // is copied here, every later one by the previous step's Euler launch
+  HIPCK(hipMemsetAsync(c.b.kstep, 0, 64 * sizeof(int), c.st));
+  RC(step_prep(c));
   RC(run_steps(c, a, workspace));
   HIPCK(final_where_out(a->cond, a->cond_mask, c.b.y, a->out, c.B, c.N, e->a.mel_dim, c.st));
   return 0;
 }
 
-// Reference-equivalent eager form of the old loop body, kept as the graph's capture source:
-// step_prep -> backbone -> CFG + Euler (dt and trajectory slot from the device step index) -> k++.
+// One NFE step, eager or as the graph's capture source: backbone -> CFG + Euler (dt and trajectory
+// slot from the device step index), which also copies the next step's table row into the fixed
+// per-step buffer and bumps the step index (folded: no step_begin / step_advance launches).
 static int enqueue_step(Ctx& c, const f5h_sample_args* a) {
   f5h_engine* e = c.e;
   {
     c.site = 0;
-    RC(step_prep(c));
     RC(backbone_step(c));
     EulerArgs u{};
     u.y = c.b.y;
@@ -1146,8 +1121,15 @@ static int enqueue_step(Ctx& c, const f5h_sample_args* a) {
     u.compute = e->bf;
     u.traj = nullptr;
     u.trajp = c.b.trajp;
+    const bool dit = e->a.backbone == F5H_DIT;
+    u.next_src = dit ? c.b.ada : c.b.temb;
+    u.next_stride = dit ? e->ada.Npad : e->a.dim;
+    u.next_n = dit ? (int)e->ada.Npad : e->a.dim;
+    u.next_dst = dit ? c.b.ada_cur : c.b.temb_cur;
+    u.nfe = c.nfe;
+    u.arrive = reinterpret_cast<unsigned*>(c.b.kstep + kArrive);
+    u.tick = e->ptick;
     KCK(cfg_euler(u, c.st));
-    KCK(step_advance(c.b.kstep, e->ptick, c.st));
   }
   return 0;
 }
@@ -1169,7 +1151,6 @@ static int run_steps(Ctx& c, const f5h_sample_args* a, const void* ws) {
   key.probe = e->probe_class;
   const bool split = e->split_cfg == 1 || (e->split_cfg == 2 && c.B >= 4);
   key.split = split;
-  key.lnf = e->ln_fuse;
   key.kernel_epoch = g_kernel_epoch.load();
   std::memcpy(&key.cfg_bits, &a->cfg_strength, 4);
   std::shared_ptr<GraphEntry> hold;  // keeps the replayed graph alive through the launch loop
@@ -1348,7 +1329,6 @@ int f5h_forward(f5h_engine* e, void* stream, const f5h_forward_args* a, void* wo
   }
   HIPCK(pack_y(e->bf, a->x, c.B * c.N, e->a.mel_dim, c.b.ypad, c.st));
   HIPCK(hipMemsetAsync(c.b.kstep, 0, sizeof(int), c.st));
-  HIPCK(hipMemsetAsync(c.b.lncnt, 0, lncnt_words((size_t)c.S * c.L) * sizeof(uint32_t), c.st));
   auto body = [](Ctx& cc) -> int {
     cc.site = 0;
     RC(step_prep(cc));
@@ -1369,7 +1349,6 @@ int f5h_forward(f5h_engine* e, void* stream, const f5h_forward_args* a, void* wo
     key.use_cfg = c.use_cfg;
     key.batch_mask = c.batch_mask;
     key.probe = e->probe_class;
-    key.lnf = e->ln_fuse;
     key.kernel_epoch = g_kernel_epoch.load();
     std::shared_ptr<GraphEntry> hold;
     RC(graph_get(c, key, false, body, hold, 1));
@@ -1457,14 +1436,6 @@ int f5h_set_cfg_streams(f5h_engine* e, int32_t n) {
   return 0;
 }
 
-int f5h_set_ln_fuse(f5h_engine* e, int32_t on) {
-  if (!e) return fail(F5H_EINVAL, "null engine");
-  if (on != 0 && on != 1) return fail(F5H_EINVAL, "ln fuse must be 0 or 1");
-  std::lock_guard<std::mutex> g(e->gm);
-  e->ln_fuse = on;
-  return 0;
-}
-
 int f5h_graph_stats(f5h_engine* e, int64_t* captures, int64_t* replays, int32_t* cached) {
   if (!e) return fail(F5H_EINVAL, "null engine");
   std::lock_guard<std::mutex> g(e->gm);
@@ -1509,8 +1480,8 @@ int f5h_op_linear(void* stream, int32_t compute, int32_t M, int32_t N, int32_t K
 }
 
 int f5h_gemm_force_config(int32_t cfg) {
-  if (cfg != -1 && cfg != 0 && cfg != 1 && cfg != 5 && cfg != 11 && (cfg < 40 || cfg > 45))
-    return fail(F5H_EINVAL, "gemm config must be -1, 0, 1, 5, 11 or 40-45");
+  if (cfg != -1 && cfg != 0 && cfg != 1 && cfg != 5 && cfg != 11)
+    return fail(F5H_EINVAL, "gemm config must be -1, 0, 1, 5 or 11");
   gemm_force_config(cfg);
   g_kernel_epoch.fetch_add(1);
   return 0;

@@ -22,7 +22,6 @@
 #pragma once
 #include "common.h"
 #include "kernels.h"
-#include "lnrow.h"
 
 #include <cstdio>
 #include <cstdlib>
@@ -115,81 +114,6 @@ F5H_DEV V8 load8(const f16* p) {
   const f16x8 v = *reinterpret_cast<const f16x8*>(p);
   return V8{{(float)v[0], (float)v[1], (float)v[2], (float)v[3], (float)v[4], (float)v[5], (float)v[6], (float)v[7]}};
 }
-// 8 consecutive 16-bit values stored write-through (sc1: the line leaves this XCD's L2 for memory),
-// for bytes another workgroup of the same launch reads (cdna_hip_programming.md Guideline 16, R1).
-// base: the first byte the descriptor covers, bytes: its extent, off: byte offset of the 16 B.
-template <typename TC>
-F5H_DEV void store8_wt(const void* base, int bytes, int off, const V8& x) {
-  typedef unsigned u32v4 __attribute__((ext_vector_type(4)));
-  typedef typename Op16<TC>::v8 v8;
-  const v8 b = {from_f32<TC>(x.v[0]), from_f32<TC>(x.v[1]), from_f32<TC>(x.v[2]), from_f32<TC>(x.v[3]),
-                from_f32<TC>(x.v[4]), from_f32<TC>(x.v[5]), from_f32<TC>(x.v[6]), from_f32<TC>(x.v[7])};
-  const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, bytes, 0x00020000);
-  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32v4, b), r, off, 0, 16);
-}
-
-// Fused LayerNorm tail of a residual GEMM (GemmArgs::ln_cnt): rows [m0, m0 + BM) of C, complete
-// once every column tile of the row block has stored, are normalised and modulated into ln_out by
-// the block's last workgroup to finish; wave w takes rows m0 + w, m0 + w + NW, ... in batches of RB
-// (all of a batch's loads in flight before its reductions). Same row arithmetic as ln_mod_kernel.
-template <typename TC, int NV, int BM, int NW>
-F5H_DEV void ln_rows(const GemmArgs& g, int m0, int wid, int lane) {
-  constexpr int RPW = BM / NW, RB = RPW < 4 ? RPW : 4;
-  static_assert(RPW % RB == 0, "row batches");
-  const int d = g.N;
-  const float4* sh = reinterpret_cast<const float4*>(g.ln_shift);
-  const float4* sc = reinterpret_cast<const float4*>(g.ln_scale);
-  float4 a[NV], b[NV];
-#pragma unroll
-  for (int k = 0; k < NV; ++k) {
-    a[k] = sc[lane + 64 * k];
-    b[k] = sh[lane + 64 * k];
-  }
-  const TC* C = reinterpret_cast<const TC*>(g.C);
-  TC* out = reinterpret_cast<TC*>(g.ln_out);
-  for (int j0 = 0; j0 < RPW; j0 += RB) {
-    float4 v[RB][NV];
-#pragma unroll
-    for (int r = 0; r < RB; ++r) {
-      const int row = min(m0 + wid + NW * (j0 + r), g.M - 1);
-#pragma unroll
-      for (int k = 0; k < NV; ++k) v[r][k] = load4f<TC>(C + (int64_t)row * g.ldc + 4 * (lane + 64 * k));
-    }
-#pragma unroll
-    for (int r = 0; r < RB; ++r) {
-      const int row = m0 + wid + NW * (j0 + r);
-      if (row < g.M) ln_mod_row<TC, NV, true>(v[r], a, b, lane, 64 * NV, d, out + (int64_t)row * d);
-    }
-  }
-}
-
-template <typename TC, int BM, int NW>
-F5H_DEV void ln_tail(const GemmArgs& g, int m0, int ntn, int tid, uint4* lds) {
-  // every storing wave's write-through stores have completed before the workgroup arrives
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  int* flag = reinterpret_cast<int*>(lds);
-  if (tid == 0) {
-    uint32_t* cnt = g.ln_cnt + m0 / BM;
-    const uint32_t old = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const int last = old == (uint32_t)(ntn - 1);
-    if (last) {
-      __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // zero for the next launch
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // drop this CU's stale L1 lines
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    *flag = last;
-  }
-  __syncthreads();
-  if (!*flag) return;
-  const int wid = tid >> 6, lane = tid & 63;
-  switch (g.N) {
-    case 1024: ln_rows<TC, 4, BM, NW>(g, m0, wid, lane); break;
-    case 768: ln_rows<TC, 3, BM, NW>(g, m0, wid, lane); break;
-    default: ln_rows<TC, 2, BM, NW>(g, m0, wid, lane); break;  // 512 (the launcher admits no other)
-  }
-}
-
 // the residual stream's element type: fp32, or the operand dtype for EPI_RESID16
 template <typename TC, int EPI>
 using ResT = typename std::conditional<EPI == EPI_RESID16, TC, float>::type;
@@ -337,15 +261,16 @@ F5H_DEV void epi8(const GemmArgs& g, int row, int col, V8 x, const V8* pre = nul
   }
 }
 
-// wait until at most `n` of this wave's VMEM ops (n/DPS stages) are outstanding
-template <int DPS>
+// wait until at most n_stages * DPS + X of this wave's VMEM ops are outstanding (the n_stages
+// youngest stages, plus X younger non-stage loads)
+template <int DPS, int X = 0>
 F5H_DEV void wait_stages(int n_stages) {
   switch (n_stages) {
-    case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
-    case 1: asm volatile("s_waitcnt vmcnt(%0)" ::"i"(DPS) : "memory"); break;
-    case 2: asm volatile("s_waitcnt vmcnt(%0)" ::"i"(2 * DPS) : "memory"); break;
-    case 3: asm volatile("s_waitcnt vmcnt(%0)" ::"i"(3 * DPS) : "memory"); break;
-    default: asm volatile("s_waitcnt vmcnt(%0)" ::"i"(4 * DPS) : "memory"); break;
+    case 0: asm volatile("s_waitcnt vmcnt(%0)" ::"i"(X) : "memory"); break;
+    case 1: asm volatile("s_waitcnt vmcnt(%0)" ::"i"(DPS + X) : "memory"); break;
+    case 2: asm volatile("s_waitcnt vmcnt(%0)" ::"i"(2 * DPS + X) : "memory"); break;
+    case 3: asm volatile("s_waitcnt vmcnt(%0)" ::"i"(3 * DPS + X) : "memory"); break;
+    default: asm volatile("s_waitcnt vmcnt(%0)" ::"i"(4 * DPS + X) : "memory"); break;
   }
 }
 
@@ -356,11 +281,8 @@ F5H_DEV void wait_stages(int n_stages) {
 // + 144 AGPR = 260: one block per CU, so the C2 QKV GEMM (480 tiles) ran as two rounds on 256 CUs
 // (tools/timeline_c2.py: second half of the grid entering 24 us after the first). Declaring 2 waves
 // per SIMD it fits in 212 VGPR, no spill.
-// RD > 0: register-staged operand intake (below) instead of the LDS-DMA ring; NS is then the number
-// of LDS slots (2).
-template <typename TC, int EPI, int BM, int BN, int WGM, int WGN, int NS, bool FAST = false, int KB = 128, int RD = 0,
-          int OCC = 2>
-__global__ __launch_bounds__(64 * WGM * WGN, OCC) void gemm_kernel(GemmArgs g) {
+template <typename TC, int EPI, int BM, int BN, int WGM, int WGN, int NS, bool FAST = false, int KB = 128>
+__global__ __launch_bounds__(64 * WGM * WGN, 2) void gemm_kernel(GemmArgs g) {
   const ProbeT probe_t = probe_enter(g.probe);
   typedef GemmCfg<BM, BN, WGM, WGN, NS, KB> C;
   constexpr int E = elems16<TC>();
@@ -443,12 +365,16 @@ __global__ __launch_bounds__(64 * WGM * WGN, OCC) void gemm_kernel(GemmArgs g) {
 #pragma unroll
     for (int j = 0; j < NT; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  // EPI_RESID: the residual rows this lane's epilogue reads are fetched before the K loop (the
-  // oldest VMEM ops, retired by the first stage wait), so the epilogue's read-modify-write does
-  // not expose a dependent HBM/MALL round trip. Register budget: small tiles only.
+  const int nk = g.K / BKE;
+  for (int p = 0; p < NS - 1 && p < nk; ++p) stage(p, p * BKE);
+  asm volatile("" ::: "memory");  // the residual loads below stay behind the stage DMA
+  // EPI_RESID: the residual rows this lane's epilogue reads are fetched right behind the first
+  // operand stages (so they do not delay stage 0: the first wait leaves them in flight, the second
+  // retires them), and the epilogue's read-modify-write does not expose a dependent HBM/MALL round
+  // trip. Register budget: small tiles only.
   constexpr int CH_ = WN / 8, TPS = 16 * CH_ / 64;
   constexpr bool PREF = (EPI == EPI_RESID || EPI == EPI_RESID16) && is16<TC>() && (16 * CH_) % 64 == 0 &&
-                        MT * TPS * 8 <= 32 && RD == 0;  // the register-staged form needs those VGPRs
+                        MT * TPS * 8 <= 32;
   V8 pre[PREF ? MT : 1][PREF ? TPS : 1];
   if constexpr (PREF) {
     const ResT<TC, EPI>* Cp = reinterpret_cast<const ResT<TC, EPI>*>(g.resid ? g.resid : g.C);
@@ -462,148 +388,20 @@ __global__ __launch_bounds__(64 * WGM * WGN, OCC) void gemm_kernel(GemmArgs g) {
         const int idx = t * 64 + lane, rr = idx / CH_, cc = idx % CH_;
         const int row = m0 + wm * WM + i * 16 + rr, col = n0 + wn * WN + cc * 8;
         const bool ok = row < g.M && col + 8 <= g.N && g.ldc % 4 == 0;
-        pre[i][t] = ok ? load8(Cp + (int64_t)row * g.ldc + col) : V8{};
+        // unconditional (a select on the address, no branch): the four loads issue back to back
+        // (a branch per load made hipcc wait for each one in turn); unused when !ok
+        pre[i][t] = load8(Cp + (ok ? (int64_t)row * g.ldc + col : 0));
       }
   }
 
-  const int nk = g.K / BKE;
-  if constexpr (RD > 0) {
-    // ---- register-staged intake: each wave keeps RD K-stages of its share of the tile's loads in
-    // flight in VGPRs (RD x (AR + BR) x 16 B per lane) and writes stage kt+1 into the other of two
-    // LDS slots while stage kt is consumed (cdna_hip_programming.md T14: issue early, write late).
-    // The bytes a CU has in flight are no longer capped by the LDS ring (Little's law: intake =
-    // bytes in flight / latency). Same LDS image and fragment reads as the LDS-DMA ring, so every
-    // accumulator sees the same operands in the same order (bitwise identical).
-    static_assert(NS == 2 && SLABS == 2, "two LDS slots of K64 stages");
-    constexpr int NL = AR + BR;
-    u32x4 rg[RD * NL];
-    // buffer loads: one 32-bit lane offset per chunk for every stage (the stage's K offset is the
-    // scalar offset), instead of a 64-bit address per chunk and stage
-    const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc(const_cast<TC*>(A), 0, 0x7fffffff, 0x00020000);
-    const __amdgpu_buffer_rsrc_t ra2 =
-        __builtin_amdgcn_make_buffer_rsrc(const_cast<TC*>(A2 ? A2 : A), 0, 0x7fffffff, 0x00020000);
-    const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc(const_cast<TC*>(W), 0, 0x7fffffff, 0x00020000);
-    int aof[AR], bof[BR];
-#pragma unroll
-    for (int i = 0; i < AR; ++i) aof[i] = (int)aoff[i] * (int)sizeof(TC);
-#pragma unroll
-    for (int i = 0; i < BR; ++i) bof[i] = (int)boff[i] * (int)sizeof(TC);
-    auto gload = [&](auto RI, int k0) {
-      u32x4* r = rg + decltype(RI)::value * NL;
-      const bool second = A2 && k0 >= g.k_split;
-      const int ka = (second ? k0 - g.k_split : k0) * (int)sizeof(TC);
-      static_for<0, AR>([&](auto I) {
-        constexpr int i = decltype(I)::value;
-        r[i] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(second ? ra2 : ra, aof[i], ka, 0));
-      });
-      static_for<0, BR>([&](auto I) {
-        constexpr int i = decltype(I)::value;
-        r[AR + i] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rw, bof[i], k0 * (int)sizeof(TC), 0));
-      });
-    };
-    auto lwrite = [&](auto RI, int slot) {
-      const u32x4* r = rg + decltype(RI)::value * NL;
-      u32x4* As = reinterpret_cast<u32x4*>(lds + slot * stage_u4);
-      u32x4* Bs = As + BM * CPR;
-      static_for<0, AR>([&](auto I) {
-        constexpr int i = decltype(I)::value;
-        As[(i * NW + wid) * 64 + lane] = r[i];
-      });
-      static_for<0, BR>([&](auto I) {
-        constexpr int i = decltype(I)::value;
-        Bs[(i * NW + wid) * 64 + lane] = r[AR + i];
-      });
-    };
-    // one K-stage: fragments of slot kt&1, then (WRITE) stage kt+1 into the other slot from its
-    // registers and (LOAD) stage kt+1+RD into the freed registers, then the MFMAs
-    auto body = [&](int kt, auto J, auto WRITE, auto LOAD) {
-      constexpr int j = decltype(J)::value;
-      constexpr bool wr = decltype(WRITE)::value, ld = decltype(LOAD)::value;
-      constexpr int rn = (j + 1) % RD;  // register slot of stage kt+1 (kt = RD*b + j)
-      const uint32_t soff = (uint32_t)((kt & 1) * C::stage_bytes);
-      u32x4 ar[SLABS][MT], br[SLABS][NT];
-#pragma unroll
-      for (int s = 0; s < SLABS; ++s) {
-        static_for<0, MT>([&](auto I) {
-          constexpr int i = decltype(I)::value;
-          ar[s][i] = lds_read_b128<i * 16 * KB>(abase[s] + soff);
-        });
-        static_for<0, NT>([&](auto Jn) {
-          constexpr int jn = decltype(Jn)::value;
-          br[s][jn] = lds_read_b128<jn * 16 * KB>(bbase[s] + soff);
-        });
-      }
-      asm volatile("s_waitcnt lgkmcnt(%0)" ::"i"(MT + NT) : "memory");  // slab 0 landed
-#pragma unroll
-      for (int i = 0; i < MT; ++i) asm volatile("" : "+v"(ar[0][i]));
-#pragma unroll
-      for (int jn = 0; jn < NT; ++jn) asm volatile("" : "+v"(br[0][jn]));
-      __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-      for (int i = 0; i < MT; ++i)
-#pragma unroll
-        for (int jn = 0; jn < NT; ++jn)
-          acc[i][jn] = Slab<TC>::mma(__builtin_bit_cast(frag, ar[0][i]), __builtin_bit_cast(frag, br[0][jn]), acc[i][jn]);
-      __builtin_amdgcn_sched_barrier(0);
-      asm volatile("" ::: "memory");  // the slot writes below stay behind the fragment reads
-      if constexpr (wr) lwrite(std::integral_constant<int, rn>{}, (kt + 1) & 1);
-      if constexpr (ld) gload(std::integral_constant<int, rn>{}, (kt + 1 + RD) * BKE);
-      constexpr int NW_ = wr ? NL : 0;  // LDS writes issued after the fragment reads
-      static_assert(NL <= 15, "lgkmcnt range");
-      asm volatile("s_waitcnt lgkmcnt(%0)" ::"i"(NW_) : "memory");  // slab 1 landed
-#pragma unroll
-      for (int i = 0; i < MT; ++i) asm volatile("" : "+v"(ar[1][i]));
-#pragma unroll
-      for (int jn = 0; jn < NT; ++jn) asm volatile("" : "+v"(br[1][jn]));
-      __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-      for (int i = 0; i < MT; ++i)
-#pragma unroll
-        for (int jn = 0; jn < NT; ++jn)
-          acc[i][jn] = Slab<TC>::mma(__builtin_bit_cast(frag, ar[1][i]), __builtin_bit_cast(frag, br[1][jn]), acc[i][jn]);
-      __builtin_amdgcn_sched_barrier(0);
-      // stage kt+1's slot writes (every wave's) are published by this barrier; it also retires
-      // every read of slot kt&1 before iteration kt+1 overwrites it with stage kt+2
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_barrier();
-    };
-    using T_ = std::integral_constant<bool, true>;
-    using F_ = std::integral_constant<bool, false>;
-    // prologue: stages 0 .. RD-1 in flight; stage 0 into slot 0; stage RD into its registers
-    // (stage by stage: the in-order vmcnt accounting the loop relies on, also across the loop entry)
-    static_for<0, RD>([&](auto P) {
-      gload(P, decltype(P)::value * BKE);
-      asm volatile("" ::: "memory");
-    });
-    lwrite(std::integral_constant<int, 0>{}, 0);
-    gload(std::integral_constant<int, 0>{}, RD * BKE);
-    asm volatile("" ::: "memory");
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    probe_mark(g.probe, probe_t, 1);
-    // nk % RD == 0 and nk >= 2 RD (the launcher checks). Blocks of RD stages: the last two blocks
-    // load nothing past stage nk-1, the very last stage writes nothing.
-    int kb = 0;
-    for (; kb < nk - 2 * RD; kb += RD)
-      static_for<0, RD>([&](auto J) { body(kb + decltype(J)::value, J, T_{}, T_{}); });
-    // block nk-2RD .. nk-RD-1: loads stage kt+1+RD <= nk-1, i.e. all but its last stage
-    static_for<0, RD>([&](auto J) {
-      constexpr int j = decltype(J)::value;
-      if constexpr (j + 1 < RD) body(kb + j, J, T_{}, T_{});
-      else body(kb + j, J, T_{}, F_{});
-    });
-    kb += RD;
-    static_for<0, RD>([&](auto J) {
-      constexpr int j = decltype(J)::value;
-      if constexpr (j + 1 < RD) body(kb + j, J, T_{}, F_{});
-      else body(kb + j, J, F_{}, F_{});
-    });
-  } else {
-  for (int p = 0; p < NS - 1 && p < nk; ++p) stage(p, p * BKE);
+  constexpr int NPRE = PREF ? MT * TPS : 0;  // residual loads issued behind the first stages
   for (int kt = 0; kt < nk; ++kt) {
     // stage kt has landed for THIS wave once at most the younger in-flight stages remain;
     // the barrier then publishes every wave's part of it
-    wait_stages<DPS>(min(NS - 2, nk - 1 - kt));
+    if (kt == 0)
+      wait_stages<DPS, NPRE>(min(NS - 2, nk - 1));
+    else
+      wait_stages<DPS>(min(NS - 2, nk - 1 - kt));
     __builtin_amdgcn_s_barrier();
     if (kt == 0) probe_mark(g.probe, probe_t, 1);
     const uint32_t soff = (uint32_t)((kt % NS) * C::stage_bytes);
@@ -663,7 +461,6 @@ __global__ __launch_bounds__(64 * WGM * WGN, OCC) void gemm_kernel(GemmArgs g) {
                                   acc[i][j]);
     }
   }
-  }  // LDS-DMA ring
   __syncthreads();
   probe_mark(g.probe, probe_t, 2);
 
@@ -785,16 +582,7 @@ __global__ __launch_bounds__(64 * WGM * WGN, OCC) void gemm_kernel(GemmArgs g) {
               const V8& c = PREF ? pre[PREF ? i : 0][PREF ? t : 0] : ri.d;
 #pragma unroll
               for (int e = 0; e < 8; ++e) o.v[e] = resid_add(c.v[e], gate8.v[e], x.v[e], ri.keep);
-              bool wt = false;
-              if constexpr (is16<TC>()) {
-                if (g.ln_cnt) {  // the row block's last workgroup reads these rows back (ln_tail)
-                  store8_wt<TC>(reinterpret_cast<const TC*>(g.C) + (int64_t)m0 * g.ldc,
-                                min(BM, g.M - m0) * (int)g.ldc * (int)sizeof(TC),
-                                ((row - m0) * (int)g.ldc + col) * (int)sizeof(TC), o);
-                  wt = true;
-                }
-              }
-              if (!wt) store8<TC>(reinterpret_cast<TC*>(g.C) + (int64_t)row * g.ldc + col, o);
+              store8<TC>(reinterpret_cast<TC*>(g.C) + (int64_t)row * g.ldc + col, o);
             } else if constexpr (EPI == EPI_GELU_TANH || EPI == EPI_GELU_ERF_OP) {
 #pragma unroll
               for (int e = 0; e < 8; ++e)
@@ -813,8 +601,6 @@ __global__ __launch_bounds__(64 * WGM * WGN, OCC) void gemm_kernel(GemmArgs g) {
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
       });
     }
-    if constexpr (EPI == EPI_RESID16 && is16<TC>())
-      if (g.ln_cnt) ln_tail<TC, BM, NW>(g, m0, ntn, tid, lds);
   }
   if constexpr (!FAST_EPI) {
 #pragma unroll
@@ -1063,31 +849,20 @@ static void launch_pp(const GemmArgs& a, hipStream_t st) {
 // ping-pong geometries; none won a shape, so they are no longer built — DESIGN.md §3.)
 // Per-CU LDS-DMA intake (~37 B/clk) bounds the small tiles: bytes per MFLOP staged =
 // 64*(BM+BN)/(BM*BN) KB, so 64x128 -> 24, 128x128 -> 16, 256x256 -> 8.
-template <typename TC, int EPI, int BM, int BN, int WGM, int WGN, int NS, int KB = 128, int RD = 0, int OCC = 2>
+template <typename TC, int EPI, int BM, int BN, int WGM, int WGN, int NS, int KB = 128>
 static void launch_cfg(const GemmArgs& a, hipStream_t st) {
   const int tiles = ((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN);
   constexpr bool HOT = EPI == EPI_QKV || EPI == EPI_RESID || EPI == EPI_RESID16 || EPI == EPI_GELU_TANH ||
                        EPI == EPI_GELU_ERF_OP || EPI == EPI_STORE || EPI == EPI_STORE16;
   if constexpr (HOT) {
     if (a.N % BN == 0 && (EPI == EPI_QKV || a.ldc % 8 == 0)) {
-      hipLaunchKernelGGL((gemm_kernel<TC, EPI, BM, BN, WGM, WGN, NS, true, KB, RD, OCC>), dim3(tiles),
-                         dim3(64 * WGM * WGN), 0, st, a);
+      hipLaunchKernelGGL((gemm_kernel<TC, EPI, BM, BN, WGM, WGN, NS, true, KB>), dim3(tiles), dim3(64 * WGM * WGN), 0,
+                         st, a);
       return;
     }
   }
-  hipLaunchKernelGGL((gemm_kernel<TC, EPI, BM, BN, WGM, WGN, NS, false, KB, RD, OCC>), dim3(tiles), dim3(64 * WGM * WGN),
-                     0, st, a);
-}
-
-// register-staged intake (gemm_kernel RD > 0) where the K-stage count allows its blocked loop (a
-// multiple of RD, at least two blocks), else the LDS-DMA form of the same tile (NSD stages)
-template <typename TC, int EPI, int BM, int BN, int RD, int NSD, int OCC = 2>
-static void launch_rs(const GemmArgs& a, hipStream_t st) {
-  const int nk = a.K / 64;
-  if (a.K % 64 == 0 && nk % RD == 0 && nk >= 2 * RD)
-    launch_cfg<TC, EPI, BM, BN, 2, 2, 2, 128, RD, OCC>(a, st);
-  else
-    launch_cfg<TC, EPI, BM, BN, 2, 2, NSD>(a, st);
+  hipLaunchKernelGGL((gemm_kernel<TC, EPI, BM, BN, WGM, WGN, NS, false, KB>), dim3(tiles), dim3(64 * WGM * WGN), 0, st,
+                     a);
 }
 
 template <typename TC, int EPI>
@@ -1095,38 +870,11 @@ static hipError_t launch_t(const GemmArgs& a, hipStream_t st) {
   if (a.M == 0) return hipSuccess;
   int cfg = 0;
   if constexpr (is16<TC>()) cfg = gemm_select_cfg(a);
-  if (a.ln_cnt) {
-    // the fused LayerNorm tail runs in gemm_kernel's whole-column epilogue of EPI_RESID16 at d = 512,
-    // 768, 1024; any other case is the GEMM followed by the ln_modulate launch (same bits)
-    if (EPI != EPI_RESID16 || a.ldc != a.N || !is16<TC>()) return hipErrorInvalidValue;
-    const bool tail = cfg != 11 && a.N % 128 == 0 && (a.N == 512 || a.N == 768 || a.N == 1024);
-    if (!tail) {
-      GemmArgs b = a;
-      b.ln_cnt = nullptr;
-      const hipError_t err = launch_t<TC, EPI>(b, st);
-      if (err != hipSuccess) return err;
-      return ln_modulate(std::is_same<TC, bf16>::value ? F5H_C_BF16 : F5H_C_FP16, a.C, 1, a.M, a.N, a.ln_shift,
-                         a.ln_scale, a.ln_out, st);
-    }
-  }
   switch (cfg) {
     case 0: launch_cfg<TC, EPI, 64, 128, 2, 2, 3>(a, st); break;
     case 1: launch_cfg<TC, EPI, 128, 128, 2, 2, 2>(a, st); break;
     case 5: launch_cfg<TC, EPI, 192, 128, 2, 2, 2>(a, st); break;
     default:
-      if constexpr (is16<TC>()) {
-        switch (cfg) {  // register-staged intake (RD K-stages in flight per wave)
-          case 40: launch_rs<TC, EPI, 64, 128, 4, 3>(a, st); return hipGetLastError();
-          case 41: launch_rs<TC, EPI, 64, 128, 2, 3>(a, st); return hipGetLastError();
-          case 42: launch_rs<TC, EPI, 128, 128, 2, 2>(a, st); return hipGetLastError();
-          // one block per CU (512 VGPRs per lane): the deeper rings the two-block forms cannot hold
-          case 43: launch_rs<TC, EPI, 128, 128, 4, 2, 1>(a, st); return hipGetLastError();
-          case 44: launch_rs<TC, EPI, 192, 128, 4, 2, 1>(a, st); return hipGetLastError();
-          case 45: launch_rs<TC, EPI, 128, 128, 8, 2, 1>(a, st); return hipGetLastError();
-          // (128x128 at RD 4 and 192x128 at RD 2 spill at two blocks per CU: more than 256 VGPRs)
-          default: break;
-        }
-      }
       if constexpr (is16<TC>()) {
         if (cfg != 11 || a.K % 64) return hipErrorInvalidValue;  // ping-pong: whole K64 phases
         launch_pp<TC, EPI, 256, 256, 1, 4, 1, 3>(a, st);

@@ -61,11 +61,6 @@ struct GemmArgs {
   DevProbe probe;                  // in-kernel launch timing (null slots: off)
   const void* resid;               // EPI_RESID / EPI_RESID16 residual input (null: C)
   const void* A2; int k_split;     // A columns [k_split, K) come from A2 (same lda), e.g. cat(x, skip)
-  // EPI_RESID16 fused LayerNorm tail (ln_cnt set; ldc == N): the last tile of each row block to
-  // finish normalises and modulates the block's rows into ln_out ([M][N] operand dtype; the next
-  // sub-layer's AdaLN LayerNorm, ln_mod_row). ln_cnt: one zeroed arrival counter per row block,
-  // reset by its last arriver. Shapes the tail does not cover run as the GEMM + ln_modulate.
-  void* ln_out; const float* ln_shift; const float* ln_scale; uint32_t* ln_cnt;
 };
 
 // compute: ComputeMode (fp32 / bf16 / fp16 operands). A and W both in the operand dtype.
@@ -146,6 +141,12 @@ struct EulerArgs {
   // trajectory slot is traj + (k+1)*B*N*mel, k = *kstep (dt above is ignored)
   // trajectory base (or null) read from *trajp in the device-indexed form
   const int* kstep; const float* tgrid; float* const* trajp;
+  // the step bookkeeping folded into this launch (device-indexed form): next_dst[0..next_n) =
+  // next_src[(k+1) * next_stride ..] for k + 1 < nfe (the next step's AdaLN / time-token row), and
+  // the workgroup that arrives last on *arrive (zeroed per call) bumps *kstep and *tick once every
+  // workgroup has read k. next_dst null: no copy; arrive null: no bump.
+  const float* next_src; int64_t next_stride; int next_n; float* next_dst; int nfe;
+  unsigned* arrive; int* tick;
 };
 hipError_t cfg_euler(const EulerArgs& a, hipStream_t st);
 // host grid t[n <= 512] -> device (by kernel argument)

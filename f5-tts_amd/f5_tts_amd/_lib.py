@@ -36,7 +36,6 @@ EXPORTS = (
     "f5h_probe_timeline",
     "f5h_set_graph_mode",
     "f5h_set_cfg_streams",
-    "f5h_set_ln_fuse",
     "f5h_graph_stats",
     "f5h_op_linear",
     "f5h_op_attention",
@@ -142,8 +141,6 @@ def lib():
     L.f5h_set_graph_mode.restype = ctypes.c_int
     L.f5h_set_cfg_streams.argtypes = [vp, i32]
     L.f5h_set_cfg_streams.restype = ctypes.c_int
-    L.f5h_set_ln_fuse.argtypes = [vp, i32]
-    L.f5h_set_ln_fuse.restype = ctypes.c_int
     L.f5h_graph_stats.argtypes = [vp, ctypes.POINTER(i64), ctypes.POINTER(i64), ctypes.POINTER(i32)]
     L.f5h_graph_stats.restype = ctypes.c_int
     L.f5h_op_linear.argtypes = [vp, i32, i32, i32, i32, vp, vp, vp, vp, vp, sz]

@@ -121,12 +121,6 @@ class Engine:
         0: automatic (two chains for batches of >= 4 utterances, the default)."""
         _lib.check(_lib.lib().f5h_set_cfg_streams(self._h, int(n)), "set_cfg_streams")
 
-    def set_ln_fuse(self, on: bool):
-        """True (default): the 16-bit DiT path's out-projection and FFN2 GEMMs apply the next AdaLN
-        LayerNorm to their finished row blocks (5 launches per block); False: separate LayerNorm
-        launches. Bitwise the same results."""
-        _lib.check(_lib.lib().f5h_set_ln_fuse(self._h, int(bool(on))), "set_ln_fuse")
-
     def graph_stats(self):
         cap, rep, n = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int32()
         _lib.check(_lib.lib().f5h_graph_stats(self._h, ctypes.byref(cap), ctypes.byref(rep), ctypes.byref(n)),

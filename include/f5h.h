@@ -194,11 +194,6 @@ int f5h_set_graph_mode(f5h_engine* eng, int32_t mode);
  * more utterances; env F5H_SPLIT_CFG=0/1/2 = never/always/auto at engine creation). Results are
  * bitwise identical. */
 int f5h_set_cfg_streams(f5h_engine* eng, int32_t n);
-/* LayerNorm launches of the 16-bit DiT path: 1 (default; env F5H_LN_FUSE=0 at creation sets 0) =
- * the out-projection and FFN2 GEMMs normalise and modulate each finished row block themselves (the
- * block's last workgroup, after an arrival count), so a DiT block is 5 launches; 0 = a separate
- * ln_mod launch before QKV and FFN1. Results are bitwise identical. */
-int f5h_set_ln_fuse(f5h_engine* eng, int32_t on);
 int f5h_graph_stats(f5h_engine* eng, int64_t* captures, int64_t* replays, int32_t* cached);
 
 /* Op-level entry points (parity tests / microbenchmarks). Device pointers, row-major. */
@@ -213,8 +208,7 @@ int f5h_op_attention(void* stream, int32_t compute, int32_t S, int32_t H, int32_
                      void* workspace, size_t workspace_bytes);
 
 /* Tuning/test hook: pin the 16-bit GEMM tile configuration for all later launches in this
- * process (0, 1, 5, 11; 40-42 register-staged intake), or -1 to restore the
- * automatic per-shape choice. */
+ * process (0, 1, 5, 11), or -1 to restore the automatic per-shape choice. */
 int f5h_gemm_force_config(int32_t cfg);
 
 /* ---------------------------------------------------------------------------------------

@@ -19,9 +19,7 @@ SHAPES = {  # name: (M, N, K); C2 = 2 x 1876 rows, C3 = 64 x 1876 rows
 for _k in (128, 256, 512, 2048, 4096):  # K sweeps at the C2 output shapes: fixed cost per launch = intercept
     SHAPES[f"c2_out_k{_k}"] = (3752, 1024, _k)
     SHAPES[f"c2_qkv_k{_k}"] = (3752, 3072, _k)
-CFGS = {0: (64, 128, 256), 1: (128, 128, 256), 5: (192, 128, 256), 11: (256, 256, 512),
-        40: (64, 128, 256), 41: (64, 128, 256), 42: (128, 128, 256),  # 40-45: register-staged intake
-        43: (128, 128, 256), 44: (192, 128, 256), 45: (128, 128, 256)}
+CFGS = {0: (64, 128, 256), 1: (128, 128, 256), 5: (192, 128, 256), 11: (256, 256, 512)}
 # round 2 also timed 8-wave one-block-per-CU tiles (128x256, 192x256, 256x128, 128x128, 256x256, 256x192),
 # K32-stage deep rings (64x128..128x256) and DMA issue interleaved with the MFMAs; all slower at C2
 # (profiles/r02_gemm_tune_c2*.txt), so they are no longer built.
