@@ -274,6 +274,194 @@ F5H_DEV void wait_stages(int n_stages) {
   }
 }
 
+// 16 bytes stored through a buffer descriptor: offsets past its extent are dropped by the hardware
+// range check, so out-of-range rows need no branch around the store
+F5H_DEV void store16_rs(__amdgpu_buffer_rsrc_t r, uint32_t off, u32x4 v) {
+  __builtin_amdgcn_raw_buffer_store_b128(v, r, off, 0, 0);
+}
+template <typename TC>
+F5H_DEV void store8_rs(__amdgpu_buffer_rsrc_t r, uint32_t elem, const V8& x) {
+  if constexpr (is16<TC>()) {
+    typedef typename Op16<TC>::v8 v8;
+    const v8 b = {from_f32<TC>(x.v[0]), from_f32<TC>(x.v[1]), from_f32<TC>(x.v[2]), from_f32<TC>(x.v[3]),
+                  from_f32<TC>(x.v[4]), from_f32<TC>(x.v[5]), from_f32<TC>(x.v[6]), from_f32<TC>(x.v[7])};
+    store16_rs(r, elem * 2u, __builtin_bit_cast(u32x4, b));
+  } else {
+    store16_rs(r, elem * 4u, u32x4{__float_as_uint(x.v[0]), __float_as_uint(x.v[1]), __float_as_uint(x.v[2]),
+                                   __float_as_uint(x.v[3])});
+    store16_rs(r, elem * 4u + 16u, u32x4{__float_as_uint(x.v[4]), __float_as_uint(x.v[5]), __float_as_uint(x.v[6]),
+                                         __float_as_uint(x.v[7])});
+  }
+}
+F5H_DEV __amdgpu_buffer_rsrc_t rsrc_of(const void* p, uint64_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), 0, (int)(uint32_t)bytes, 0x00020000);
+}
+
+// Fast epilogue of one wave's sub-tile (whole-column tiles of the hot epilogues), per 16-row strip:
+// accumulators -> the wave's LDS strip (fp32, EPAD-float rows) -> 8-column chunks of whole rows. A lane's
+// column chunk is the same in every strip, so bias/gate/QKV head indices are loaded once, and the row
+// data of strip i+1 (RoPE pairs, residual rows, row-mask bytes) is fetched before strip i stores.
+// The strip loop has no control flow: bias presence is a template choice, per-lane choices (RoPE on
+// this column, rows past M) are selects or the store descriptor's range check. Any branch or any
+// arithmetic on a just-loaded value makes hipcc wait for that load, and on gfx9 every store issued
+// before it counts in the same vmcnt: at C3 such waits made the 256x256 ping-pong epilogue 13-15 us per
+// tile (profiles/r03_timeline_c3.txt). rbase/cbase: the sub-tile's first row/column.
+// Shared by gemm_kernel and gemm_pp_kernel.
+template <typename TC, int EPI, int MT, int NT, int WN, int EPAD, bool PREF, bool BIAS, int PM, int PT>
+F5H_DEV void epilogue_fast_t(const GemmArgs& g, const f32x4 (&acc)[MT][NT], float* Cs, int rbase, int cbase,
+                             int lane, const V8 (&pre)[PM][PT]) {
+  constexpr int CH = WN / 8;          // 8-column chunks per strip row
+  constexpr int TPC = 16 * CH / 64;   // chunks per lane per strip
+  static_assert(64 % CH == 0 && (16 * CH) % 64 == 0, "whole chunks per lane");
+  const int fr = lane & 15, q = lane >> 4;
+  const int cc = lane % CH;
+  const int col = cbase + cc * 8;
+  V8 bias8 = V8{};
+  if constexpr (BIAS) bias8 = load8(g.bias + col);
+  V8 gate8 = V8{{1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f}};
+  if constexpr (EPI == EPI_RESID || EPI == EPI_RESID16)
+    if (g.gate) gate8 = load8(g.gate + col);
+  int which = 0, head = 0, dh = 0;
+  bool rope_on = false;
+  float qsc = 1.f;
+  __amdgpu_buffer_rsrc_t dst;
+  if constexpr (EPI == EPI_QKV) {
+    // a wave's 64 columns are one head of one of q/k/v (cbase % 64 == 0): wave-uniform, so the
+    // destination descriptor lives in scalar registers (a per-lane one costs a waterfall loop per store)
+    static_assert(WN == 64, "one head per wave");
+    const int inner = g.heads * 64;
+    which = __builtin_amdgcn_readfirstlane(fdiv(cbase, inner));
+    const int hc = col - which * inner;
+    head = hc >> 6;
+    dh = hc & 63;
+    rope_on = which < 2 && head < g.rope_heads;
+    qsc = (which == 0 && g.q_scale != 0.f) ? g.q_scale : 1.f;
+    dst = rsrc_of(which == 0 ? g.q : (which == 1 ? g.k : g.v), (uint64_t)g.M * inner * sizeof(TC));
+  } else {
+    constexpr int OES = (EPI == EPI_STORE || EPI == EPI_RESID) ? 4 : (int)sizeof(TC);
+    dst = rsrc_of(g.C, (uint64_t)g.M * g.ldc * OES);
+  }
+  // Loads only, raw bits, no arithmetic on their results here (see above): conversions happen at the
+  // use, one strip later. Row indices are clamped instead of branched on (rows >= M are never stored).
+  struct RowIn {
+    u32x4 d0, d1;  // RoPE (cos, sin) of four pairs (QKV, fp32) or the residual row chunk (RESID)
+    uint32_t kb;   // RESID row-mask byte
+  };
+  const __amdgpu_buffer_rsrc_t rk = rsrc_of(g.rowkeep, g.rowkeep ? (uint64_t)g.M : 0);  // null: reads 0
+  const bool masked = g.rowkeep != nullptr;
+  auto fetch = [&](int i, RowIn (&ri)[TPC]) {
+#pragma unroll
+    for (int t = 0; t < TPC; ++t) {
+      const int rr = t * (64 / CH) + lane / CH;
+      const int rowc = min(rbase + i * 16 + rr, g.M - 1);
+      if constexpr (EPI == EPI_QKV) {
+        const int pos = rowc - fdiv(rowc, g.seq_len) * g.seq_len;
+        const u32x4* p = reinterpret_cast<const u32x4*>(g.rope + (int64_t)pos * 32 + (dh >> 1));
+        ri[t].d0 = p[0];
+        ri[t].d1 = p[1];
+      } else if constexpr (EPI == EPI_RESID || EPI == EPI_RESID16) {
+        if constexpr (!PREF) {
+          const u32x4* p = reinterpret_cast<const u32x4*>(reinterpret_cast<const ResT<TC, EPI>*>(
+                                                              g.resid ? g.resid : g.C) + (int64_t)rowc * g.ldc + col);
+          ri[t].d0 = p[0];
+          if constexpr (sizeof(ResT<TC, EPI>) == 4) ri[t].d1 = p[1];  // fp32 rows: 32 B
+        }
+        ri[t].kb = __builtin_amdgcn_raw_buffer_load_b8(rk, (uint32_t)rowc, 0, 0);
+      }
+    }
+  };
+  // the raw row data as 8 fp32 values
+  auto as_v8 = [&](const RowIn& ri) -> V8 {
+    if constexpr (EPI == EPI_RESID16 && is16<TC>()) {
+      typedef typename Op16<TC>::v8 v8;
+      const v8 h = __builtin_bit_cast(v8, ri.d0);
+      return V8{{to_f32(h[0]), to_f32(h[1]), to_f32(h[2]), to_f32(h[3]), to_f32(h[4]), to_f32(h[5]), to_f32(h[6]),
+                 to_f32(h[7])}};
+    } else {
+      return V8{{__uint_as_float(ri.d0[0]), __uint_as_float(ri.d0[1]), __uint_as_float(ri.d0[2]),
+                 __uint_as_float(ri.d0[3]), __uint_as_float(ri.d1[0]), __uint_as_float(ri.d1[1]),
+                 __uint_as_float(ri.d1[2]), __uint_as_float(ri.d1[3])}};
+    }
+  };
+  RowIn rbuf[2][TPC];
+  fetch(0, rbuf[0]);
+  static_for<0, MT>([&](auto I) {
+    constexpr int i = decltype(I)::value;
+    if constexpr (i + 1 < MT) fetch(i + 1, rbuf[(i + 1) & 1]);
+#pragma unroll
+    for (int j = 0; j < NT; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) Cs[(q * 4 + r) * EPAD + j * 16 + fr] = acc[i][j][r];
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+    for (int t = 0; t < TPC; ++t) {
+      const int rr = t * (64 / CH) + lane / CH;
+      const int row = rbase + i * 16 + rr;  // rows >= M: dropped by the store descriptor
+      const float* src = Cs + rr * EPAD + cc * 8;
+      const float4 a0 = *reinterpret_cast<const float4*>(src), a1 = *reinterpret_cast<const float4*>(src + 4);
+      V8 x{{a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w}};
+      if constexpr (BIAS) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) x.v[e] = add_nc(x.v[e], bias8.v[e]);
+      }
+      const RowIn& ri = rbuf[i & 1][t];
+      if constexpr (EPI == EPI_QKV) {
+        const V8 cs = as_v8(ri);
+#pragma unroll
+        for (int pr = 0; pr < 2; ++pr) {
+          const float c0 = cs.v[4 * pr + 0], s0 = cs.v[4 * pr + 1];
+          const float c1 = cs.v[4 * pr + 2], s1 = cs.v[4 * pr + 3];
+          const float a0_ = x.v[4 * pr + 0], a1_ = x.v[4 * pr + 1], b0 = x.v[4 * pr + 2], b1 = x.v[4 * pr + 3];
+          const float r0 = rope_re(a0_, a1_, c0, s0), r1 = rope_im(a0_, a1_, c0, s0);
+          const float r2 = rope_re(b0, b1, c1, s1), r3 = rope_im(b0, b1, c1, s1);
+          x.v[4 * pr + 0] = rope_on ? r0 : a0_;
+          x.v[4 * pr + 1] = rope_on ? r1 : a1_;
+          x.v[4 * pr + 2] = rope_on ? r2 : b0;
+          x.v[4 * pr + 3] = rope_on ? r3 : b1;
+        }
+#pragma unroll
+        for (int e = 0; e < 8; ++e) x.v[e] = mul_nc(x.v[e], qsc);  // exact for qsc = 1 (k, v columns)
+        const int sq = fdiv(row, g.seq_len), pos = row - sq * g.seq_len;
+        store8_rs<TC>(dst, (uint32_t)((((int64_t)sq * g.heads + head) * g.seq_len + pos) * 64 + dh), x);
+      } else if constexpr (EPI == EPI_RESID || EPI == EPI_RESID16) {
+        V8 c;
+        if constexpr (PREF)
+          c = pre[PREF ? i : 0][PREF ? t : 0];
+        else
+          c = as_v8(ri);
+        const float keep = (!masked || ri.kb) ? 1.f : 0.f;
+        V8 o;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) o.v[e] = resid_add(c.v[e], gate8.v[e], x.v[e], keep);
+        store8_rs<ResT<TC, EPI>>(dst, (uint32_t)((int64_t)row * g.ldc + col), o);
+      } else if constexpr (EPI == EPI_GELU_TANH || EPI == EPI_GELU_ERF_OP) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e)
+          x.v[e] = EPI == EPI_GELU_ERF_OP ? gelu_erf(x.v[e])
+                                          : (is16<TC>() ? gelu_tanh_fast(x.v[e]) : gelu_tanh(x.v[e]));
+        store8_rs<TC>(dst, (uint32_t)((int64_t)row * g.ldc + col), x);
+      } else if constexpr (EPI == EPI_STORE16) {
+        store8_rs<TC>(dst, (uint32_t)((int64_t)row * g.ldc + col), x);
+      } else {  // EPI_STORE
+        store8_rs<float>(dst, (uint32_t)((int64_t)row * g.ldc + col), x);
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  });
+}
+template <typename TC, int EPI, int MT, int NT, int WN, int EPAD, bool PREF, int PM, int PT>
+F5H_DEV void epilogue_fast(const GemmArgs& g, const f32x4 (&acc)[MT][NT], float* Cs, int rbase, int cbase,
+                           int lane, const V8 (&pre)[PM][PT]) {
+  if (g.bias)
+    epilogue_fast_t<TC, EPI, MT, NT, WN, EPAD, PREF, true>(g, acc, Cs, rbase, cbase, lane, pre);
+  else
+    epilogue_fast_t<TC, EPI, MT, NT, WN, EPAD, PREF, false>(g, acc, Cs, rbase, cbase, lane, pre);
+}
+
 // FAST: the launcher guarantees whole-column tiles (N % BN == 0, ldc % 8 == 0) for the hot
 // epilogues, so the epilogue is compiled without per-element column guards (see below).
 // Launch bounds: two 4-wave blocks per CU (2 waves per SIMD) must fit the register file, i.e. <= 256
@@ -461,6 +649,10 @@ __global__ __launch_bounds__(64 * WGM * WGN, 2) void gemm_kernel(GemmArgs g) {
                                   acc[i][j]);
     }
   }
+  // the K loop's last wait was vmcnt(0) (hand-written, invisible to hipcc): say so with the builtin,
+  // so hipcc does not wait again (behind the epilogue's own stores) before the first use of a value
+  // loaded before the loop (the residual prefetch)
+  __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0), expcnt/lgkmcnt untouched
   __syncthreads();
   probe_mark(g.probe, probe_t, 2);
 
@@ -477,130 +669,7 @@ __global__ __launch_bounds__(64 * WGM * WGN, 2) void gemm_kernel(GemmArgs g) {
   // chunk; measured 9.5 us of a 30.6 us QKV launch before).
   constexpr bool FAST_EPI = FAST && (64 % CH == 0) && (16 * CH) % 64 == 0;
   if constexpr (FAST_EPI) {
-    {
-      const int cc = lane % CH;
-      const int col = n0 + wn * WN + cc * 8;
-      V8 bias8 = g.bias ? load8(g.bias + col) : V8{};
-      V8 gate8 = V8{{1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f}};
-      if constexpr (EPI == EPI_RESID || EPI == EPI_RESID16)
-        if (g.gate) gate8 = load8(g.gate + col);
-      int which = 0, head = 0, dh = 0;
-      bool rope_on = false;
-      float qsc = 1.f;
-      TC* qkv_dst = nullptr;
-      if constexpr (EPI == EPI_QKV) {
-        const int inner = g.heads * 64;
-        which = fdiv(col, inner);
-        const int hc = col - which * inner;
-        head = hc >> 6;
-        dh = hc & 63;
-        rope_on = which < 2 && head < g.rope_heads;
-        qsc = (which == 0 && g.q_scale != 0.f) ? g.q_scale : 1.f;
-        qkv_dst = reinterpret_cast<TC*>(which == 0 ? g.q : (which == 1 ? g.k : g.v));
-      }
-      struct RowIn {
-        V8 d;         // RoPE (cos, sin) of two pairs (QKV) or the residual row chunk (RESID)
-        float keep;   // RESID row mask
-      };
-      auto fetch = [&](int i, RowIn (&ri)[TPC]) {
-#pragma unroll
-        for (int t = 0; t < TPC; ++t) {
-          const int rr = t * (64 / CH) + lane / CH;
-          const int row = m0 + wm * WM + i * 16 + rr;
-          const bool ok = row < g.M;
-          ri[t].keep = 1.f;
-          if constexpr (EPI == EPI_QKV) {
-            ri[t].d = V8{};
-            if (ok && rope_on) {
-              const int pos = row - fdiv(row, g.seq_len) * g.seq_len;
-              ri[t].d = load8(reinterpret_cast<const float*>(g.rope + (int64_t)pos * 32 + (dh >> 1)));
-            }
-          } else if constexpr (EPI == EPI_RESID || EPI == EPI_RESID16) {
-            if constexpr (PREF) {
-              ri[t].d = V8{};
-            } else {
-              ri[t].d = ok ? load8(reinterpret_cast<const ResT<TC, EPI>*>(g.resid ? g.resid : g.C) + (int64_t)row * g.ldc + col) : V8{};
-            }
-            if (ok && g.rowkeep && !g.rowkeep[row]) ri[t].keep = 0.f;
-          } else {
-            ri[t].d = V8{};
-          }
-        }
-      };
-      RowIn rbuf[2][TPC];
-      fetch(0, rbuf[0]);
-      static_for<0, MT>([&](auto I) {
-        constexpr int i = decltype(I)::value;
-        if constexpr (i + 1 < MT) fetch(i + 1, rbuf[(i + 1) & 1]);
-#pragma unroll
-        for (int j = 0; j < NT; ++j)
-#pragma unroll
-          for (int r = 0; r < 4; ++r) Cs[(q * 4 + r) * C::EPAD + j * 16 + fr] = acc[i][j][r];
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-#pragma unroll
-        for (int t = 0; t < TPC; ++t) {
-          const int rr = t * (64 / CH) + lane / CH;
-          const int row = m0 + wm * WM + i * 16 + rr;
-          const float* src = Cs + rr * C::EPAD + cc * 8;
-          const float4 a0 = *reinterpret_cast<const float4*>(src), a1 = *reinterpret_cast<const float4*>(src + 4);
-          V8 x{{a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w}};
-          if (g.bias) {
-#pragma unroll
-            for (int e = 0; e < 8; ++e) x.v[e] = add_nc(x.v[e], bias8.v[e]);
-          }
-          const RowIn& ri = rbuf[i & 1][t];
-          if (row < g.M) {
-            if constexpr (EPI == EPI_QKV) {
-              if (rope_on) {
-#pragma unroll
-                for (int pr = 0; pr < 2; ++pr) {
-                  const float c0 = ri.d.v[4 * pr + 0], s0 = ri.d.v[4 * pr + 1];
-                  const float c1 = ri.d.v[4 * pr + 2], s1 = ri.d.v[4 * pr + 3];
-                  const float a0_ = x.v[4 * pr + 0], a1_ = x.v[4 * pr + 1], b0 = x.v[4 * pr + 2], b1 = x.v[4 * pr + 3];
-                  x.v[4 * pr + 0] = rope_re(a0_, a1_, c0, s0);
-                  x.v[4 * pr + 1] = rope_im(a0_, a1_, c0, s0);
-                  x.v[4 * pr + 2] = rope_re(b0, b1, c1, s1);
-                  x.v[4 * pr + 3] = rope_im(b0, b1, c1, s1);
-                }
-              }
-              if (qsc != 1.f) {
-#pragma unroll
-                for (int e = 0; e < 8; ++e) x.v[e] = mul_nc(x.v[e], qsc);
-              }
-              const int sq = fdiv(row, g.seq_len), pos = row - sq * g.seq_len;
-              store8<TC>(qkv_dst + (((int64_t)sq * g.heads + head) * g.seq_len + pos) * 64 + dh, x);
-            } else if constexpr (EPI == EPI_RESID) {
-              const V8& c = PREF ? pre[PREF ? i : 0][PREF ? t : 0] : ri.d;
-              V8 o;
-#pragma unroll
-              for (int e = 0; e < 8; ++e) o.v[e] = resid_add(c.v[e], gate8.v[e], x.v[e], ri.keep);
-              store8<float>(reinterpret_cast<float*>(g.C) + (int64_t)row * g.ldc + col, o);
-            } else if constexpr (EPI == EPI_RESID16) {
-              V8 o;
-              const V8& c = PREF ? pre[PREF ? i : 0][PREF ? t : 0] : ri.d;
-#pragma unroll
-              for (int e = 0; e < 8; ++e) o.v[e] = resid_add(c.v[e], gate8.v[e], x.v[e], ri.keep);
-              store8<TC>(reinterpret_cast<TC*>(g.C) + (int64_t)row * g.ldc + col, o);
-            } else if constexpr (EPI == EPI_GELU_TANH || EPI == EPI_GELU_ERF_OP) {
-#pragma unroll
-              for (int e = 0; e < 8; ++e)
-                x.v[e] = EPI == EPI_GELU_ERF_OP ? gelu_erf(x.v[e])
-                                                : (is16<TC>() ? gelu_tanh_fast(x.v[e]) : gelu_tanh(x.v[e]));
-              store8<TC>(reinterpret_cast<TC*>(g.C) + (int64_t)row * g.ldc + col, x);
-            } else if constexpr (EPI == EPI_STORE16) {
-              store8<TC>(reinterpret_cast<TC*>(g.C) + (int64_t)row * g.ldc + col, x);
-            } else {  // EPI_STORE
-              store8<float>(reinterpret_cast<float*>(g.C) + (int64_t)row * g.ldc + col, x);
-            }
-          }
-        }
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-      });
-    }
+    epilogue_fast<TC, EPI, MT, NT, WN, C::EPAD, PREF>(g, acc, Cs, m0 + wm * WM, n0 + wn * WN, lane, pre);
   }
   if constexpr (!FAST_EPI) {
 #pragma unroll
@@ -669,7 +738,7 @@ struct PPCfg {
   static_assert(bytes <= 160 * 1024, "LDS");
 };
 
-template <typename TC, int EPI, int BM, int BN, int WGM2, int WGN2, int KS, int D>
+template <typename TC, int EPI, int BM, int BN, int WGM2, int WGN2, int KS, int D, bool FAST = false>
 __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(GemmArgs g) {
   const ProbeT probe_t = probe_enter(g.probe);
   typedef PPCfg<BM, BN, WGM2, WGN2, KS, D> C;
@@ -811,6 +880,12 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(GemmArgs g) {
   float* Cs = reinterpret_cast<float*>(lds) + wid * 16 * C::EPAD;
   constexpr int CH = WN / 8;
   const int rbase = m0 + grp * (BM / 2) + wm * WM, cbase = n0 + wn * WN;
+  if constexpr (FAST) {
+    // whole-column tiles: the strip-pipelined epilogue (the generic one below waits out every strip's
+    // residual / RoPE loads before its stores: 13-15 us per 256x256 tile at C3, profiles/r03_timeline_c3.txt)
+    const V8 none[1][1] = {};
+    epilogue_fast<TC, EPI, MT, NT, WN, C::EPAD, false>(g, acc, Cs, rbase, cbase, lane, none);
+  } else {
 #pragma unroll
   for (int i = 0; i < MT; ++i) {
 #pragma unroll
@@ -831,12 +906,28 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(GemmArgs g) {
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   }
+  }
   probe_exit(g.probe, probe_t);
+}
+
+// the fast epilogue: whole-column tiles, 16-B aligned rows, destinations a buffer descriptor covers
+template <int EPI>
+static bool fast_epi_ok(const GemmArgs& a, int BN) {
+  const uint64_t span = (uint64_t)a.M * (uint64_t)std::max<int64_t>(a.ldc, a.N) * 4;
+  return a.N % BN == 0 && (EPI == EPI_QKV || a.ldc % 8 == 0) && span < 0xFFFFFFFFull;
 }
 
 template <typename TC, int EPI, int BM, int BN, int WGM2, int WGN2, int KS, int D>
 static void launch_pp(const GemmArgs& a, hipStream_t st) {
   const int tiles = ((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN);
+  constexpr bool HOT = EPI == EPI_QKV || EPI == EPI_RESID || EPI == EPI_RESID16 || EPI == EPI_GELU_TANH ||
+                       EPI == EPI_GELU_ERF_OP || EPI == EPI_STORE || EPI == EPI_STORE16;
+  if constexpr (HOT) {
+    if (fast_epi_ok<EPI>(a, BN)) {
+      hipLaunchKernelGGL((gemm_pp_kernel<TC, EPI, BM, BN, WGM2, WGN2, KS, D, true>), dim3(tiles), dim3(512), 0, st, a);
+      return;
+    }
+  }
   hipLaunchKernelGGL((gemm_pp_kernel<TC, EPI, BM, BN, WGM2, WGN2, KS, D>), dim3(tiles), dim3(512), 0, st, a);
 }
 
@@ -855,7 +946,7 @@ static void launch_cfg(const GemmArgs& a, hipStream_t st) {
   constexpr bool HOT = EPI == EPI_QKV || EPI == EPI_RESID || EPI == EPI_RESID16 || EPI == EPI_GELU_TANH ||
                        EPI == EPI_GELU_ERF_OP || EPI == EPI_STORE || EPI == EPI_STORE16;
   if constexpr (HOT) {
-    if (a.N % BN == 0 && (EPI == EPI_QKV || a.ldc % 8 == 0)) {
+    if (fast_epi_ok<EPI>(a, BN)) {
       hipLaunchKernelGGL((gemm_kernel<TC, EPI, BM, BN, WGM, WGN, NS, true, KB>), dim3(tiles), dim3(64 * WGM * WGN), 0,
                          st, a);
       return;
