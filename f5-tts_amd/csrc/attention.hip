@@ -212,7 +212,10 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn16_kernel(AttnArgs a) {
 #pragma unroll
       for (int ks = 1; ks < 4; ++ks) sacc[t] = OP::mma32(__builtin_bit_cast(v8, kf[t][ks]), qf[ks], sacc[t]);
     }
+    // both halves of V^T now: their LDS latency hides under the row max and the first exp2 chunk (read
+    // after the max, hipcc hoisted the exp2s above them and the wait before the first PV MFMA exposed it)
     vread(std::integral_constant<int, 0>{});
+    vread(std::integral_constant<int, 1>{});
     if (kt * 64 + 64 > klen) {  // ragged last tile: keys past klen get p = 0
       const int kbase = kt * 64 + 4 * h;
 #pragma unroll
@@ -271,7 +274,6 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn16_kernel(AttnArgs a) {
         oacc[u] = OP::mma32(__builtin_bit_cast(v8, w), pf[t][sx], oacc[u]);
       }
     };
-    vread(std::integral_constant<int, 1>{});
     exp_chunk(std::integral_constant<int, 0>{});
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 #pragma unroll

@@ -241,6 +241,12 @@ template <typename T> F5H_DEV constexpr int elems16() { return 16 / (int)sizeof(
 // Compile-time loop: f(integral_constant<int, I>) for I in [B, E). Register arrays indexed
 // through it are split into scalars by SROA (a runtime-indexed or loop-indexed array can
 // be lowered to scratch before the unroller runs).
+// raw buffer descriptor over [p, p + bytes): loads past the extent read 0, stores past it are dropped
+// (the hardware range check), so out-of-range lanes need no branch; bytes < 2^32
+F5H_DEV __amdgpu_buffer_rsrc_t rsrc_of(const void* p, uint64_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), 0, (int)(uint32_t)bytes, 0x00020000);
+}
+
 template <int B, int E, typename F>
 F5H_DEV void static_for(F&& f) {
   if constexpr (B < E) {

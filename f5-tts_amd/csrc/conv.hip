@@ -14,45 +14,79 @@
 
 namespace f5h {
 
-// Mish epilogue of one 8-channel row chunk (shared by both kernels): bias, row mask, Mish, then the
-// operand-dtype store (mode 0), or the residual added in fp32 and stored as fp32 (mode 1) or in the
-// operand dtype (mode 2: the 16-bit residual stream).
-template <typename TC>
-F5H_DEV void conv_epi8(const ConvArgs& a, const float* c, int s, int pos, int oc, bool keep) {
-  const int d = a.d;
-  float v[8];
+// Epilogue of a conv block from its [BP][CP] fp32 LDS image: IT 8-channel row chunks per thread at a
+// fixed column (c8 = (tid & 7) * 8). Everything the chunks read (bias, row-mask bytes, residual rows)
+// is loaded before any chunk is stored: a load issued after a store waits for it (gfx9 counts stores
+// in vmcnt), and the former per-element bias loads under the row-mask branch waited one by one.
+template <typename TC, int BP, int NT, int CP, int MODE>
+F5H_DEV void conv_epilogue(const ConvArgs& a, const float* Cs, int tid, int s, int n0, int grp, int cg) {
+  constexpr int IT = BP * 8 / NT;
+  static_assert(IT * NT == BP * 8 && NT % 8 == 0, "whole chunk passes");
+  const int L = a.L, d = a.d;
+  const int c8 = (tid & 7) * 8, oc = grp * cg + c8;
+  if (c8 >= cg) return;  // (groups narrower than 64 channels)
+  const float4 b0 = *reinterpret_cast<const float4*>(a.bias + oc), b1 = *reinterpret_cast<const float4*>(a.bias + oc + 4);
+  const __amdgpu_buffer_rsrc_t rk = rsrc_of(a.rowkeep, a.rowkeep ? (uint64_t)a.S * L : 0);
+  uint32_t kb[IT];
+  float4 r0[IT], r1[IT];
 #pragma unroll
-  for (int e = 0; e < 8; ++e) {
-    const float x = keep ? c[e] + a.bias[oc + e] : 0.f;
-    v[e] = is16<TC>() ? mish_fast(x) : mish(x);
+  for (int it = 0; it < IT; ++it) {
+    const int pos = min(n0 + (tid >> 3) + it * (NT / 8), L - 1);
+    kb[it] = __builtin_amdgcn_raw_buffer_load_b8(rk, (uint32_t)(s * L + pos), 0, 0);
+    if constexpr (MODE != 0) {
+      const float* rs = a.resid + ((int64_t)s * L + pos) * d + oc;
+      r0[it] = *reinterpret_cast<const float4*>(rs);
+      r1[it] = *reinterpret_cast<const float4*>(rs + 4);
+    }
   }
-  if (a.mode == 0) {
-    TC* y = reinterpret_cast<TC*>(a.y) + ((int64_t)s * a.L + pos) * d + oc;
-    if constexpr (is16<TC>()) {
-      typename Op16<TC>::v8 o = {from_f32<TC>(v[0]), from_f32<TC>(v[1]), from_f32<TC>(v[2]), from_f32<TC>(v[3]),
-                                 from_f32<TC>(v[4]), from_f32<TC>(v[5]), from_f32<TC>(v[6]), from_f32<TC>(v[7])};
-      *reinterpret_cast<typename Op16<TC>::v8*>(y) = o;
+  const float bb[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
+#pragma unroll
+  for (int it = 0; it < IT; ++it) {
+    const int row = (tid >> 3) + it * (NT / 8), pos = n0 + row;
+    if (pos >= L) continue;
+    const bool keep = !a.rowkeep || kb[it] != 0;
+    const float* c = Cs + row * CP + c8;
+    float v[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const float x = keep ? c[e] + bb[e] : 0.f;
+      v[e] = is16<TC>() ? mish_fast(x) : mish(x);
+    }
+    if constexpr (MODE == 0) {
+      TC* y = reinterpret_cast<TC*>(a.y) + ((int64_t)s * L + pos) * d + oc;
+      if constexpr (is16<TC>()) {
+        typename Op16<TC>::v8 o = {from_f32<TC>(v[0]), from_f32<TC>(v[1]), from_f32<TC>(v[2]), from_f32<TC>(v[3]),
+                                   from_f32<TC>(v[4]), from_f32<TC>(v[5]), from_f32<TC>(v[6]), from_f32<TC>(v[7])};
+        *reinterpret_cast<typename Op16<TC>::v8*>(y) = o;
+      } else {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) y[e] = from_f32<TC>(v[e]);
+      }
+    } else if constexpr (MODE == 2) {
+      if constexpr (is16<TC>()) {
+        TC* y = reinterpret_cast<TC*>(a.y) + ((int64_t)s * a.y_seq_stride + a.y_row_off + pos) * d + oc;
+        typename Op16<TC>::v8 o = {
+            from_f32<TC>(v[0] + r0[it].x), from_f32<TC>(v[1] + r0[it].y), from_f32<TC>(v[2] + r0[it].z),
+            from_f32<TC>(v[3] + r0[it].w), from_f32<TC>(v[4] + r1[it].x), from_f32<TC>(v[5] + r1[it].y),
+            from_f32<TC>(v[6] + r1[it].z), from_f32<TC>(v[7] + r1[it].w)};
+        *reinterpret_cast<typename Op16<TC>::v8*>(y) = o;
+      }
     } else {
-#pragma unroll
-      for (int e = 0; e < 8; ++e) y[e] = from_f32<TC>(v[e]);
+      float* y = reinterpret_cast<float*>(a.y) + ((int64_t)s * a.y_seq_stride + a.y_row_off + pos) * d + oc;
+      *reinterpret_cast<float4*>(y) = make_float4(v[0] + r0[it].x, v[1] + r0[it].y, v[2] + r0[it].z, v[3] + r0[it].w);
+      *reinterpret_cast<float4*>(y + 4) =
+          make_float4(v[4] + r1[it].x, v[5] + r1[it].y, v[6] + r1[it].z, v[7] + r1[it].w);
     }
-  } else if (a.mode == 2) {
-    if constexpr (is16<TC>()) {
-      const float* rs = a.resid + ((int64_t)s * a.L + pos) * d + oc;
-      const float4 r0 = *reinterpret_cast<const float4*>(rs), r1 = *reinterpret_cast<const float4*>(rs + 4);
-      TC* y = reinterpret_cast<TC*>(a.y) + ((int64_t)s * a.y_seq_stride + a.y_row_off + pos) * d + oc;
-      typename Op16<TC>::v8 o = {from_f32<TC>(v[0] + r0.x), from_f32<TC>(v[1] + r0.y), from_f32<TC>(v[2] + r0.z),
-                                 from_f32<TC>(v[3] + r0.w), from_f32<TC>(v[4] + r1.x), from_f32<TC>(v[5] + r1.y),
-                                 from_f32<TC>(v[6] + r1.z), from_f32<TC>(v[7] + r1.w)};
-      *reinterpret_cast<typename Op16<TC>::v8*>(y) = o;
-    }
-  } else {
-    float* y = reinterpret_cast<float*>(a.y) + ((int64_t)s * a.y_seq_stride + a.y_row_off + pos) * d + oc;
-    const float* rs = a.resid + ((int64_t)s * a.L + pos) * d + oc;
-    const float4 r0 = *reinterpret_cast<const float4*>(rs), r1 = *reinterpret_cast<const float4*>(rs + 4);
-    *reinterpret_cast<float4*>(y) = make_float4(v[0] + r0.x, v[1] + r0.y, v[2] + r0.z, v[3] + r0.w);
-    *reinterpret_cast<float4*>(y + 4) = make_float4(v[4] + r1.x, v[5] + r1.y, v[6] + r1.z, v[7] + r1.w);
   }
+}
+template <typename TC, int BP, int NT, int CP>
+F5H_DEV void conv_epilogue_any(const ConvArgs& a, const float* Cs, int tid, int s, int n0, int grp, int cg) {
+  if (a.mode == 0)
+    conv_epilogue<TC, BP, NT, CP, 0>(a, Cs, tid, s, n0, grp, cg);
+  else if (a.mode == 2)
+    conv_epilogue<TC, BP, NT, CP, 2>(a, Cs, tid, s, n0, grp, cg);
+  else
+    conv_epilogue<TC, BP, NT, CP, 1>(a, Cs, tid, s, n0, grp, cg);
 }
 
 template <int N>
@@ -177,12 +211,7 @@ __global__ __launch_bounds__(128 * NWM, 1) void conv_kernel(ConvArgs a) {
       for (int r = 0; r < 4; ++r)
         Cs[(wm * 32 + i * 16 + (lane >> 4) * 4 + r) * CP + wn * 32 + j * 16 + (lane & 15)] = acc[i][j][r];
   __syncthreads();
-  for (int c = tid; c < BP * 8; c += NT) {
-    const int row = c >> 3, c8 = (c & 7) * 8, pos = n0 + row;
-    if (pos >= L || c8 >= cg) continue;
-    const bool keep = !a.rowkeep || a.rowkeep[(int64_t)s * L + pos];
-    conv_epi8<TC>(a, Cs + row * CP + c8, s, pos, grp * cg + c8, keep);
-  }
+  conv_epilogue_any<TC, BP, NT, CP>(a, Cs, tid, s, n0, grp, cg);
 }
 
 // Input-window image: fragment reads take rows t + 16i + (lane & 15) for every tap t, so the
@@ -227,8 +256,11 @@ __global__ __launch_bounds__(512, 1) void conv16_kernel(ConvArgs a) {
   {
     constexpr int NIT = (WROWS * CPR + NT - 1) / NT;
     constexpr int EPC = 16 / sizeof(TX);  // TX elements per 16-B load; 8 channels = 1 (16-bit) or 2 (fp32) loads
+    // (no branch around any load: hipcc would wait for each conditional one in turn)
     uint4 raw[NIT][8 / EPC];
+    uint32_t kb[NIT];
     bool okv[NIT];
+    const __amdgpu_buffer_rsrc_t rk = rsrc_of(a.rowkeep, a.rowkeep ? (uint64_t)a.S * L : 0);
 #pragma unroll
     for (int it = 0; it < NIT; ++it) {
       const int idx = tid + it * NT, row = idx / CPR, ch = idx % CPR;
@@ -237,14 +269,12 @@ __global__ __launch_bounds__(512, 1) void conv16_kernel(ConvArgs a) {
       okv[it] = idx < WROWS * CPR && q >= 0 && q < L && ch * 8 < cg;
       const uint4* src = reinterpret_cast<const uint4*>(X + ((int64_t)s * L + qc) * d + grp * cg + cc);
 #pragma unroll
-      for (int h = 0; h < 8 / EPC; ++h) raw[it][h] = idx < WROWS * CPR ? src[h] : make_uint4(0, 0, 0, 0);
+      for (int h = 0; h < 8 / EPC; ++h) raw[it][h] = src[h];  // in range for every idx (clamped row)
+      kb[it] = __builtin_amdgcn_raw_buffer_load_b8(rk, (uint32_t)(s * L + qc), 0, 0);
     }
     if (a.rowkeep) {
 #pragma unroll
-      for (int it = 0; it < NIT; ++it) {
-        const int idx = tid + it * NT, q = n0 - 15 + idx / CPR;
-        if (okv[it]) okv[it] = a.rowkeep[(int64_t)s * L + q] != 0;
-      }
+      for (int it = 0; it < NIT; ++it) okv[it] = okv[it] && kb[it] != 0;
     }
 #pragma unroll
     for (int it = 0; it < NIT; ++it) {
@@ -386,12 +416,7 @@ __global__ __launch_bounds__(512, 1) void conv16_kernel(ConvArgs a) {
       for (int r = 0; r < 4; ++r)
         Cs[(wm * 64 + i * 16 + (lane >> 4) * 4 + r) * CP + wn * 32 + j * 16 + (lane & 15)] = acc[i][j][r];
   __syncthreads();
-  for (int c = tid; c < BP * 8; c += NT) {
-    const int row = c >> 3, c8 = (c & 7) * 8, pos = n0 + row;
-    if (pos >= L || c8 >= cg) continue;
-    const bool keep = !a.rowkeep || a.rowkeep[(int64_t)s * L + pos];
-    conv_epi8<TC>(a, Cs + row * CP + c8, s, pos, grp * cg + c8, keep);
-  }
+  conv_epilogue_any<TC, BP, NT, CP>(a, Cs, tid, s, n0, grp, cg);
 }
 
 hipError_t conv_pos(int compute, const ConvArgs& a, hipStream_t st) {

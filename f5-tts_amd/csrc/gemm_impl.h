@@ -293,9 +293,6 @@ F5H_DEV void store8_rs(__amdgpu_buffer_rsrc_t r, uint32_t elem, const V8& x) {
                                          __float_as_uint(x.v[7])});
   }
 }
-F5H_DEV __amdgpu_buffer_rsrc_t rsrc_of(const void* p, uint64_t bytes) {
-  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), 0, (int)(uint32_t)bytes, 0x00020000);
-}
 
 // Fast epilogue of one wave's sub-tile (whole-column tiles of the hot epilogues), per 16-row strip:
 // accumulators -> the wave's LDS strip (fp32, EPAD-float rows) -> 8-column chunks of whole rows. A lane's
