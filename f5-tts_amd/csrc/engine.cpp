@@ -498,7 +498,7 @@ static void layout(const f5h_engine* e, WS& ws, Bufs& b, int B, int N, int nfe, 
   b.v = ws.take<char>(rows * inner * es);
   b.o = ws.take<char>(rows * inner * es);
   b.f = ws.take<char>(rows * a.ff_dim * es);
-  b.p = ws.take<float>(rows * a.mel_dim);
+  b.p = ws.take<float>(rows * e->proj_out.Npad);  // proj_out rows padded to the GEMM tile width
   b.rope = ws.take<float2>((size_t)L * 32);
   b.rowkeep = ws.take<uint8_t>(rows);
   b.kvlen = ws.take<int32_t>(S);
@@ -834,7 +834,11 @@ static int backbone_part(Ctx& c, int s0, int ns, hipStream_t st) {
   } else {
     KCK(rms_norm_g(bf, h, r16, rows, d, e->norm_out_g, aop, st));
   }
-  GemmArgs g = gargs(aop, d, e->proj_out, rows, b.p + ro * a.mel_dim, a.mel_dim);
+  // all Npad (128) columns: the padded weight rows and bias are zero, and whole-column tiles take the
+  // fast epilogue; readers use the first mel_dim columns of each 128-float row
+  const int pld = e->proj_out.Npad;
+  GemmArgs g = gargs(aop, d, e->proj_out, rows, b.p + ro * pld, pld);
+  g.N = pld;
   KCK(gemm(bf, EPI_STORE, g, st));
   return 0;
 }
@@ -1109,9 +1113,9 @@ static int enqueue_step(Ctx& c, const f5h_sample_args* a) {
     u.N = c.N;
     u.mel = e->a.mel_dim;
     u.p = c.b.p;
-    u.p_seq_stride = (int64_t)c.L * e->a.mel_dim;
+    u.p_seq_stride = (int64_t)c.L * e->proj_out.Npad;
     u.p_row_off = e->a.backbone == F5H_DIT ? 0 : 1;
-    u.p_ld = e->a.mel_dim;
+    u.p_ld = e->proj_out.Npad;
     u.use_cfg = c.use_cfg;
     u.cfg = a->cfg_strength;
     u.dt = 0.f;
@@ -1357,7 +1361,7 @@ int f5h_forward(f5h_engine* e, void* stream, const f5h_forward_args* a, void* wo
   } else {
     RC(body(c));
   }
-  HIPCK(copy_pred(c.b.p, c.S, c.L, e->a.backbone == F5H_DIT ? 0 : 1, e->a.mel_dim, e->a.mel_dim, a->pred, c.st));
+  HIPCK(copy_pred(c.b.p, c.S, c.L, e->a.backbone == F5H_DIT ? 0 : 1, e->a.mel_dim, e->proj_out.Npad, a->pred, c.st));
   return 0;
 }
 

@@ -335,13 +335,14 @@ F5H_DEV void epilogue_fast_t(const GemmArgs& g, const f32x4 (&acc)[MT][NT], floa
     qsc = (which == 0 && g.q_scale != 0.f) ? g.q_scale : 1.f;
     dst = rsrc_of(which == 0 ? g.q : (which == 1 ? g.k : g.v), (uint64_t)g.M * inner * sizeof(TC));
   } else {
-    constexpr int OES = (EPI == EPI_STORE || EPI == EPI_RESID) ? 4 : (int)sizeof(TC);
-    dst = rsrc_of(g.C, (uint64_t)g.M * g.ldc * OES);
+    constexpr int OES = (EPI == EPI_STORE || EPI == EPI_RESID || EPI == EPI_INPROJ) ? 4 : (int)sizeof(TC);
+    dst = rsrc_of(g.C, (uint64_t)(g.M + (EPI == EPI_INPROJ ? g.dual_rows : 0)) * g.ldc * OES);
   }
   // Loads only, raw bits, no arithmetic on their results here (see above): conversions happen at the
   // use, one strip later. Row indices are clamped instead of branched on (rows >= M are never stored).
   struct RowIn {
-    u32x4 d0, d1;  // RoPE (cos, sin) of four pairs (QKV, fp32) or the residual row chunk (RESID)
+    u32x4 d0, d1;  // RoPE (cos, sin) of four pairs (QKV, fp32), the residual row chunk (RESID), the addend (INPROJ)
+    u32x4 e0, e1;  // INPROJ: the second output row's addend
     uint32_t kb;   // RESID row-mask byte
   };
   const __amdgpu_buffer_rsrc_t rk = rsrc_of(g.rowkeep, g.rowkeep ? (uint64_t)g.M : 0);  // null: reads 0
@@ -364,6 +365,13 @@ F5H_DEV void epilogue_fast_t(const GemmArgs& g, const f32x4 (&acc)[MT][NT], floa
           if constexpr (sizeof(ResT<TC, EPI>) == 4) ri[t].d1 = p[1];  // fp32 rows: 32 B
         }
         ri[t].kb = __builtin_amdgcn_raw_buffer_load_b8(rk, (uint32_t)rowc, 0, 0);
+      } else if constexpr (EPI == EPI_INPROJ) {
+        const u32x4* p = reinterpret_cast<const u32x4*>(g.add + (int64_t)rowc * g.ld_add + col);
+        ri[t].d0 = p[0];
+        ri[t].d1 = p[1];
+        const u32x4* p2 = reinterpret_cast<const u32x4*>(g.add + (int64_t)(rowc + g.dual_rows) * g.ld_add + col);
+        ri[t].e0 = p2[0];  // (rows [M, M + dual_rows) of the addend; the first rows again when dual_rows = 0)
+        ri[t].e1 = p2[1];
       }
     }
   };
@@ -441,6 +449,22 @@ F5H_DEV void epilogue_fast_t(const GemmArgs& g, const f32x4 (&acc)[MT][NT], floa
         store8_rs<TC>(dst, (uint32_t)((int64_t)row * g.ldc + col), x);
       } else if constexpr (EPI == EPI_STORE16) {
         store8_rs<TC>(dst, (uint32_t)((int64_t)row * g.ldc + col), x);
+      } else if constexpr (EPI == EPI_INPROJ) {
+        // x.W_x^T + P for this branch's row, and for the other branch's row (same x, dit.py:162)
+        V8 o0, o1;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          o0.v[e] = x.v[e] + __uint_as_float(ri.d0[e]);
+          o0.v[e + 4] = x.v[e + 4] + __uint_as_float(ri.d1[e]);
+          o1.v[e] = x.v[e] + __uint_as_float(ri.e0[e]);
+          o1.v[e + 4] = x.v[e + 4] + __uint_as_float(ri.e1[e]);
+        }
+        // rows >= M would land in the second block: drop them explicitly (an offset past the descriptor's
+        // extent, which fast_epi_ok keeps below 0xF0000000 bytes; no 32-bit wrap for either 16-B half)
+        constexpr uint32_t kPast = 0xF0000000u / 4;
+        store8_rs<float>(dst, row < g.M ? (uint32_t)((int64_t)row * g.ldc + col) : kPast, o0);
+        if (g.dual_rows)
+          store8_rs<float>(dst, row < g.M ? (uint32_t)((int64_t)(row + g.dual_rows) * g.ldc + col) : kPast, o1);
       } else {  // EPI_STORE
         store8_rs<float>(dst, (uint32_t)((int64_t)row * g.ldc + col), x);
       }
@@ -910,15 +934,16 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(GemmArgs g) {
 // the fast epilogue: whole-column tiles, 16-B aligned rows, destinations a buffer descriptor covers
 template <int EPI>
 static bool fast_epi_ok(const GemmArgs& a, int BN) {
-  const uint64_t span = (uint64_t)a.M * (uint64_t)std::max<int64_t>(a.ldc, a.N) * 4;
-  return a.N % BN == 0 && (EPI == EPI_QKV || a.ldc % 8 == 0) && span < 0xFFFFFFFFull;
+  const uint64_t span = (uint64_t)(a.M + a.dual_rows) * (uint64_t)std::max<int64_t>(a.ldc, a.N) * 4;
+  return a.N % BN == 0 && (EPI == EPI_QKV || a.ldc % 8 == 0) && (EPI != EPI_INPROJ || a.ld_add % 8 == 0) &&
+         span < 0xF0000000ull;
 }
 
 template <typename TC, int EPI, int BM, int BN, int WGM2, int WGN2, int KS, int D>
 static void launch_pp(const GemmArgs& a, hipStream_t st) {
   const int tiles = ((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN);
   constexpr bool HOT = EPI == EPI_QKV || EPI == EPI_RESID || EPI == EPI_RESID16 || EPI == EPI_GELU_TANH ||
-                       EPI == EPI_GELU_ERF_OP || EPI == EPI_STORE || EPI == EPI_STORE16;
+                       EPI == EPI_GELU_ERF_OP || EPI == EPI_STORE || EPI == EPI_STORE16 || EPI == EPI_INPROJ;
   if constexpr (HOT) {
     if (fast_epi_ok<EPI>(a, BN)) {
       hipLaunchKernelGGL((gemm_pp_kernel<TC, EPI, BM, BN, WGM2, WGN2, KS, D, true>), dim3(tiles), dim3(512), 0, st, a);
@@ -941,7 +966,7 @@ template <typename TC, int EPI, int BM, int BN, int WGM, int WGN, int NS, int KB
 static void launch_cfg(const GemmArgs& a, hipStream_t st) {
   const int tiles = ((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN);
   constexpr bool HOT = EPI == EPI_QKV || EPI == EPI_RESID || EPI == EPI_RESID16 || EPI == EPI_GELU_TANH ||
-                       EPI == EPI_GELU_ERF_OP || EPI == EPI_STORE || EPI == EPI_STORE16;
+                       EPI == EPI_GELU_ERF_OP || EPI == EPI_STORE || EPI == EPI_STORE16 || EPI == EPI_INPROJ;
   if constexpr (HOT) {
     if (fast_epi_ok<EPI>(a, BN)) {
       hipLaunchKernelGGL((gemm_kernel<TC, EPI, BM, BN, WGM, WGN, NS, true, KB>), dim3(tiles), dim3(64 * WGM * WGN), 0,
