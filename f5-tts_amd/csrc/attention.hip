@@ -11,8 +11,8 @@
 //     THR (log2 units) p = exp2(s - m_run) needs no subtraction and O is never rescaled
 //     (P <= 2^THR). A wave that sees a larger jump re-bases: m_run += d, O, l *= 2^-d, s -= d
 //     (cdna_hip_programming.md T13; the branch is forced by the spike tests).
-//   * row sums on the matrix pipe: l^T += ones . P^T (4 extra MFMAs per tile instead of 32 VALU
-//     adds), summed from the same 16-bit P that enters O.
+//   * row sums on the VALU from the fp32 exp2s: 16 packed adds per tile and wave, issued in the
+//     MFMA shadow with the packs (the matrix-pipe form l^T += ones . P^T cost 4 of 20 MFMAs per tile).
 //   * the QK^T chains start from a loop-carried -m_run block (rewritten only on a re-base), and P
 //     is produced in four 16-key chunks whose MFMAs are issued between the next chunk's exp2s
 //     (sched_group_barrier): on gfx950 only a wave's OWN vector work hides under its MFMAs.
@@ -152,15 +152,14 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn16_kernel(AttnArgs a) {
       vaddr[u][g8] = lds0 + 64 * 128 + r1 * 128 + swz128(r1, dh >> 3) * 16 + ((dh >> 2) & 1) * 8;
     }
 
-  const T one = from_f32<T>(1.f);
-  const v8 ones = {one, one, one, one, one, one, one, one};
+  typedef float f2 __attribute__((ext_vector_type(2)));
   float m_run = 0.f;  // running max (log2 units), valid after tile 0
-  f32x16 oacc[2], lacc, minit;  // minit: -m_run in every slot, the QK^T chains' first C operand
+  f32x16 oacc[2], minit;  // minit: -m_run in every slot, the QK^T chains' first C operand
+  f2 lrow = {0.f, 0.f};   // this lane's part of its query's row sum (packed fp32 adds)
 #pragma unroll
   for (int r = 0; r < 16; ++r) {
     oacc[0][r] = 0.f;
     oacc[1][r] = 0.f;
-    lacc[r] = 0.f;
     minit[r] = 0.f;
   }
 
@@ -248,26 +247,31 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn16_kernel(AttnArgs a) {
       for (int r = 0; r < 16; ++r) {
         oacc[0][r] *= alpha;
         oacc[1][r] *= alpha;
-        lacc[r] *= alpha;
         minit[r] = -m_run;
       }
 #pragma unroll
       for (int t = 0; t < 2; ++t)
 #pragma unroll
         for (int r = 0; r < 16; ++r) sacc[t][r] -= d;
+      lrow *= alpha;
     }
-    // exp2 / pack of 16-key chunk c = (t, sx) of P, then its three MFMAs (row sums, both O^T
-    // halves), issued between chunk c+1's exp2s and packs: a wave's own VALU work issues in the
-    // shadow of its MFMAs (per accumulator the MFMA order is unchanged)
+    // exp2 / pack of 16-key chunk c = (t, sx) of P (row sums from the fp32 exp2s, four packed
+    // adds), then its two MFMAs (both O^T halves), issued between chunk c+1's exp2s and packs: a
+    // wave's own VALU work issues in the shadow of its MFMAs (per accumulator the MFMA order is
+    // unchanged)
     v8 pf[2][2];
     auto exp_chunk = [&](auto C) {
       constexpr int t = decltype(C)::value >> 1, sx = decltype(C)::value & 1;
 #pragma unroll
-      for (int j = 0; j < 8; ++j) pf[t][sx][j] = from_f32<T>(__builtin_amdgcn_exp2f(sacc[t][8 * sx + j]));
+      for (int j = 0; j < 8; j += 2) {
+        const f2 e = {__builtin_amdgcn_exp2f(sacc[t][8 * sx + j]), __builtin_amdgcn_exp2f(sacc[t][8 * sx + j + 1])};
+        pf[t][sx][j] = from_f32<T>(e.x);
+        pf[t][sx][j + 1] = from_f32<T>(e.y);
+        lrow += e;
+      }
     };
     auto mma_chunk = [&](auto C) {
       constexpr int t = decltype(C)::value >> 1, sx = decltype(C)::value & 1;
-      lacc = OP::mma32(ones, pf[t][sx], lacc);  // row sums: l^T += ones . P^T
 #pragma unroll
       for (int u = 0; u < 2; ++u) {
         const uint4 w = make_uint4(vf[u][t][sx][0].x, vf[u][t][sx][0].y, vf[u][t][sx][1].x, vf[u][t][sx][1].y);
@@ -289,22 +293,20 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn16_kernel(AttnArgs a) {
     static_for<0, 3>([&](auto C) {
       mma_chunk(C);
       exp_chunk(std::integral_constant<int, decltype(C)::value + 1>{});
-      // per MFMA gap: 3, 3, 2 exp2 (TRANS) and 1, 1, 2 packs
+      // per MFMA gap: 4 exp2 (TRANS), 2 packs and 2 row-sum adds
       __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-      __builtin_amdgcn_sched_group_barrier(0x400, 3, 0);
-      __builtin_amdgcn_sched_group_barrier(0x002, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x400, 4, 0);
+      __builtin_amdgcn_sched_group_barrier(0x002, 4, 0);
       __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-      __builtin_amdgcn_sched_group_barrier(0x400, 3, 0);
-      __builtin_amdgcn_sched_group_barrier(0x002, 1, 0);
-      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-      __builtin_amdgcn_sched_group_barrier(0x400, 2, 0);
-      __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);
+      __builtin_amdgcn_sched_group_barrier(0x400, 4, 0);
+      __builtin_amdgcn_sched_group_barrier(0x002, 4, 0);
       __builtin_amdgcn_sched_barrier(0);
     });
     mma_chunk(std::integral_constant<int, 3>{});
   }
   probe_mark(a.probe, probe_t, 2);
-  const float l_tot = lacc[0];
+  float l_tot = lrow.x + lrow.y;
+  l_tot += xor32(l_tot);  // lanes l and l + 32 hold the two key halves of one query
   const float inv = l_tot > 0.f ? 1.f / l_tot : 0.f;
   // Epilogue (T21): lane l < 32 holds columns 8k..8k+3 of its row, lane l + 32 columns 8k+4..8k+7; one
   // permlane32 swap per dword pairs groups k and k+1, so every lane stores 16 contiguous bytes

@@ -386,15 +386,15 @@ def test_graph_eviction_never_waits_for_other_streams():
     other = torch.cuda.Stream()
     with torch.cuda.stream(other):
         torch.cuda._sleep(int(2.0e9))  # ~1 s of spinning on another stream
-    worst = 0.0
+    took = []
     for inp, y0 in cases[17:]:  # every call captures a new step graph and evicts one
         t0 = time.perf_counter()
         _run_case(m, inp, y0, steps=2)
-        worst = max(worst, time.perf_counter() - t0)
+        took.append(round(time.perf_counter() - t0, 4))
     still_busy = not other.query()
     torch.cuda.synchronize()
     assert still_busy, "the spin kernel ended before the evicting calls: raise its length"
-    assert worst < 0.3, worst
+    assert max(took) < 0.3, took
 
 
 def test_nfe_512_runs_and_matches_oracle():
