@@ -376,21 +376,29 @@ def test_graph_eviction_never_waits_for_other_streams():
     work: while a ~1 s spin kernel occupies another stream, calls with new shapes (each evicting an
     entry) return to the host long before it ends (the old eviction synchronised the device)."""
     _need_gpu()
+    import gc as pygc
     import time
 
     m = _model(gc.arch_of("tiny"), "bf16")
     cases = [_tiny_case(40 + 5 * i, i) for i in range(24)]
     for inp, y0 in cases[:17]:  # fill the cache (17 shapes: step graphs, evictions start)
         _run_case(m, inp, y0, steps=2)
+    # Engines of earlier tests still waiting for the cyclic collector are destroyed now, not inside the
+    # timed calls: releasing an engine's device memory (hipFree) synchronises the whole device.
+    pygc.collect()
     torch.cuda.synchronize()
     other = torch.cuda.Stream()
     with torch.cuda.stream(other):
         torch.cuda._sleep(int(2.0e9))  # ~1 s of spinning on another stream
     took = []
-    for inp, y0 in cases[17:]:  # every call captures a new step graph and evicts one
-        t0 = time.perf_counter()
-        _run_case(m, inp, y0, steps=2)
-        took.append(round(time.perf_counter() - t0, 4))
+    pygc.disable()
+    try:
+        for inp, y0 in cases[17:]:  # every call captures a new step graph and evicts one
+            t0 = time.perf_counter()
+            _run_case(m, inp, y0, steps=2)
+            took.append(round(time.perf_counter() - t0, 4))
+    finally:
+        pygc.enable()
     still_busy = not other.query()
     torch.cuda.synchronize()
     assert still_busy, "the spin kernel ended before the evicting calls: raise its length"
