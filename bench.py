@@ -56,20 +56,24 @@ def seq_flops(arch, N):
     return per_tok * L + 4.0 * depth * d * L * L
 
 
-def pmc_traffic(kernel_class):
+def pmc_traffic(kernel_class, shape):
     """HBM bytes per launch of a kernel class from the latest committed rocprofv3 PMC summary
     (profiles/*_pmc_classes.json, written by tools/pmc_classes.py from separate FETCH_SIZE and
     WRITE_SIZE passes: 2 x FETCH_SIZE (gfx950 counts half of wide streaming reads,
-    MI355X_MICROARCH.md §HBM) + WRITE_SIZE), and its source file."""
+    MI355X_MICROARCH.md §HBM) + WRITE_SIZE), and its source file. Only a summary measured at this
+    launch shape (`shape` = {"S", "L", "dim", "depth"}) is used; other shapes get None."""
     import glob
     files = sorted(glob.glob(os.path.join(REPO, "profiles", "*_pmc_classes.json")))
     if not files:
         return None, None
     d = json.load(open(files[-1]))
+    src = os.path.relpath(files[-1], REPO)
+    if d.get("shape") != shape:
+        return None, f"{src} is for shape {d.get('shape')}, not {shape}"
     ent = d.get("classes", {}).get(kernel_class)
     if not ent:
-        return None, os.path.relpath(files[-1], REPO)
-    return ent["hbm_bytes"], os.path.relpath(files[-1], REPO)
+        return None, src
+    return ent["hbm_bytes"], src
 
 
 def build_model(preset, compute, device):
@@ -198,7 +202,7 @@ def class_entry(kc, avg_ms, n, arch, S, L, launches_per_call, ms_call, chains=1)
         ach = by / (avg_ms * 1e-3) / 1e9 if by else 0.0
         e.update(bound="hbm", achieved=round(ach, 1), peak=PEAK_HBM_GBPS, unit="GB/s",
                  frac=round(ach / PEAK_HBM_GBPS, 4), bytes_per_launch=by)
-    traffic, src = pmc_traffic(kc)
+    traffic, src = pmc_traffic(kc, {"S": S, "L": L, "dim": arch["dim"], "depth": arch["depth"]})
     e["traffic"] = traffic
     e["traffic_source"] = src
     if traffic and kc in ("qkv", "out", "ffn1", "ffn2", "attention"):

@@ -46,3 +46,13 @@ def test_norm_bytes_follow_the_residual_width():
     assert bench.resid_bytes(dit, esz=4) == 4  # fp32 parity mode
     assert bench.class_bytes("norm", dit, S, L) == S * L * 1024 * (2 + 2)  # 15.37 MB
     assert bench.class_bytes("norm", unett, S, L) == S * L * 1024 * (4 + 2)
+
+
+def test_pmc_traffic_only_at_the_measured_shape():
+    """The committed PMC summary is attached to a bench line only at the launch shape it was measured
+    on (C2: S=2, N=1876, Base); any other shape (C3, C5, fp32 tiny) reports no traffic."""
+    c2 = {"S": 2, "L": 1876, "dim": 1024, "depth": 22}
+    t, src = bench.pmc_traffic("attention", c2)
+    assert t and t > 0 and src.startswith("profiles/")
+    t, src = bench.pmc_traffic("attention", dict(c2, S=64))
+    assert t is None and "not" in src
