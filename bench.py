@@ -185,7 +185,7 @@ PEAK_HBM_GBPS = 8000.0
 
 def class_entry(kc, avg_ms, n, arch, S, L, launches_per_call, ms_call, chains=1):
     """One kernel class: algorithmic work per launch slot / average launch span. With the two CFG
-    chains captured in parallel (chains = 2, batches of >= 4 utterances) each chain launches the class
+    chains captured in parallel (chains = 2, F5H_SPLIT_CFG=1) each chain launches the class
     on half the sequences and the two chains' launches of a class overlap in time, so a slot (the span
     of one launch) covers both halves: flops are counted for all S sequences and the slot count is per
     chain."""
@@ -289,7 +289,8 @@ def main():
 
     eng = model.transformer.get_engine(model.engine_compute(), device)
     S = 2 * B if case["cfg"] >= 1e-5 else B
-    chains = 2 if (case["cfg"] >= 1e-5 and B >= 4) else 1  # the engine's automatic CFG-branch split
+    # the engine's CFG launch chains: one packed chain unless F5H_SPLIT_CFG=1 forces the split
+    chains = 2 if (case["cfg"] >= 1e-5 and os.environ.get("F5H_SPLIT_CFG") == "1") else 1
     L = Nmax if arch["backbone"] == "DiT" else Nmax + 1
     launches = {"norm": arch["depth"]}
     for kc in ("qkv", "attention", "out", "ffn1", "ffn2"):

@@ -109,9 +109,9 @@ struct f5h_engine {
   hipStream_t cap2 = nullptr; // second capture stream: the unconditional CFG branch
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;
   int graph_mode = 1;
-  // CFG branches as parallel captured chains: 2 = auto (batches of >= 4 utterances: C5 -4 % per call;
-  // at B = 1 the half-size launches cost more than the overlap gains, C2 +4 %), 1 = always, 0 = never
-  // (env F5H_SPLIT_CFG, f5h_set_cfg_streams)
+  // CFG branches as parallel captured chains: 1 = always, 0 = never, 2 = auto, which is one packed chain:
+  // with the round-3 kernels the split measured C2 +2.3 %, C3 +1.0 %, C5 +1.0 % per call and C4 -0.7 %
+  // (profiles/r03_ab_cfg_chains.txt; in round 1 it won C5 by 4 %). Env F5H_SPLIT_CFG, f5h_set_cfg_streams.
   int split_cfg = 2;
   uint64_t use_ctr = 0;
   int64_t n_captures = 0, n_replays = 0;
@@ -1153,7 +1153,7 @@ static int run_steps(Ctx& c, const f5h_sample_args* a, const void* ws) {
   key.use_cfg = c.use_cfg;
   key.batch_mask = c.batch_mask;
   key.probe = e->probe_class;
-  const bool split = e->split_cfg == 1 || (e->split_cfg == 2 && c.B >= 4);
+  const bool split = e->split_cfg == 1;  // auto (2): one packed chain
   key.split = split;
   key.kernel_epoch = g_kernel_epoch.load();
   std::memcpy(&key.cfg_bits, &a->cfg_strength, 4);

@@ -118,7 +118,7 @@ class Engine:
 
     def set_cfg_streams(self, n: int):
         """2: the captured step runs the two CFG branches as parallel launch chains; 1: one chain;
-        0: automatic (two chains for batches of >= 4 utterances, the default)."""
+        0: automatic (the default; currently one chain, the faster form at C2, C3 and C5)."""
         _lib.check(_lib.lib().f5h_set_cfg_streams(self._h, int(n)), "set_cfg_streams")
 
     def graph_stats(self):

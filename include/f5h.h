@@ -190,9 +190,9 @@ int f5h_probe_timeline(f5h_engine* eng, uint64_t* stamps, int32_t max_wg, int32_
 int f5h_set_graph_mode(f5h_engine* eng, int32_t mode);
 /* Launch chains of the captured step: 2 captures the conditional and the unconditional CFG branch as
  * two parallel chains (fork/join by events), so kernel boundaries of one branch overlap work of the
- * other; 1 = one chain over the packed batch; 0 = automatic (default: two chains for batches of 4 or
- * more utterances; env F5H_SPLIT_CFG=0/1/2 = never/always/auto at engine creation). Results are
- * bitwise identical. */
+ * other; 1 = one chain over the packed batch; 0 = automatic (the default: currently one chain, measured
+ * faster at C2, C3 and C5 and 0.7 % slower at C4; env F5H_SPLIT_CFG=0/1/2 = never/always/auto at engine
+ * creation). Results are bitwise identical. */
 int f5h_set_cfg_streams(f5h_engine* eng, int32_t n);
 int f5h_graph_stats(f5h_engine* eng, int64_t* captures, int64_t* replays, int32_t* cached);
 

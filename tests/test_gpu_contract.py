@@ -451,7 +451,7 @@ def test_edge_sample_fp16(name):
 @pytest.mark.parametrize("compute", ["bf16", "fp32"])
 def test_cfg_branch_chains_bitwise_equal(compute):
     """The step graph with the conditional and unconditional CFG branches captured as two parallel
-    launch chains (the default for batches of >= 4 utterances) gives bitwise the result of one chain
+    launch chains (F5H_SPLIT_CFG=1 / set_cfg_streams(2)) gives bitwise the result of one chain
     over the packed batch, and of the eager launch sequence."""
     _need_gpu()
     m = _model(gc.arch_of("tiny"), compute)
