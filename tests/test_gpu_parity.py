@@ -73,10 +73,12 @@ if os.environ.get("F5H_TEST_GEMM_CFGS"):  # tuning runs: check extra configurati
 
 
 @pytest.mark.parametrize("compute", ["bf16", "fp16"])
-@pytest.mark.parametrize("M,N,K", [(3752, 3072, 1024), (77, 100, 1024), (3752, 1024, 2048), (700, 2048, 128)])
+@pytest.mark.parametrize("M,N,K", [(3752, 3072, 1024), (77, 100, 1024), (3752, 1024, 2048), (700, 2048, 128),
+                                   (16384, 4096, 1024)])
 def test_op_linear_every_tile_config(M, N, K, compute):
     """Every 16-bit tile configuration meets the fp64 reference and all of them agree bit for
-    bit (same per-element K order: one lane, k-steps in sequence)."""
+    bit (same per-element K order: one lane, k-steps in sequence). 16384 x 4096: 1,024 tiles of
+    256 x 256, the large-batch size class that picks cfg 11 by default."""
     _need_gpu()
     g = torch.Generator(device="cpu").manual_seed(M * 7 + N + K)
     A = torch.randn(M, K, generator=g).to(DEV)
