@@ -1,7 +1,7 @@
 // One row of the AdaLN LayerNorm + modulate (AdaLayerNorm modules.py:325, ff_norm :753,
 // AdaLayerNorm_Final :346): LN(x) (no affine, eps 1e-6) * (1 + scale) + shift, a wave per row, lane
-// l holding elements 4(l + 64k) .. +3. Shared by ln_mod_kernel (elementwise.hip) and the residual
-// GEMM's fused LayerNorm tail (gemm_impl.h), so both produce the same bits.
+// l holding elements 4(l + 64k) .. +3, used by ln_mod_kernel (elementwise.hip). (Round 3 also ran it as
+// a fused tail of the residual GEMMs, which needed the same bits; measured slower and removed)
 #pragma once
 #include "common.h"
 
