@@ -693,7 +693,9 @@ static int backbone_part(Ctx& c, int s0, int ns, hipStream_t st) {
   // (wrong results; bounds what removing those launches can save). Never set in tests or benches.
   static const bool skip_ln = [] {
     const char* v = getenv("F5H_DIAG_SKIP_LN");
-    return v && *v == '1';
+    const bool on = v && *v == '1';
+    if (on) std::fprintf(stderr, "[f5h] F5H_DIAG_SKIP_LN=1: LayerNorm launches skipped, results are WRONG (timing only)\n");
+    return on;
   }();
   const bool do_ln = !(skip_ln && r16);
   const size_t hsz = r16 ? es : sizeof(float);
