@@ -205,12 +205,14 @@ def class_entry(kc, avg_ms, n, arch, S, L, launches_per_call, ms_call, chains=1)
     traffic, src = pmc_traffic(kc, {"S": S, "L": L, "dim": arch["dim"], "depth": arch["depth"]})
     e["traffic"] = traffic
     e["traffic_source"] = src
-    if traffic and kc in ("qkv", "out", "ffn1", "ffn2", "attention"):
+    if traffic and kc in ("qkv", "out", "ffn1", "ffn2", "attention", "conv"):
         d, ff = arch["dim"], int(arch["dim"] * arch["ff_mult"])
         kn = {"qkv": (d, 3 * d), "out": (d, d), "ffn1": (d, ff), "ffn2": (ff, d)}.get(kc)
         if kn:  # operands + result at the operand width (residual read+write for RESID)
             K, Nn = kn
             alg = 2 * (S * L * K + Nn * K) + (2 * resid_bytes(arch) if kc in ("out", "ffn2") else 2) * S * L * Nn
+        elif kc == "conv":  # one grouped conv layer: input + output rows + weights (tools/pmc_classes.py)
+            alg = S * L * d * (2 + resid_bytes(arch)) + d * (d // 16) * 31 * 2
         else:
             alg = 4 * 2 * S * arch["heads"] * L * 64
         e["algorithmic_bytes"] = alg

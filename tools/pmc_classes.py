@@ -39,7 +39,7 @@ def classify(disp):
             for off, c in ORDER.items():
                 if 0 <= i + off < len(disp):
                     cls.setdefault(i + off, c)
-        elif "conv_kernel" in name:
+        elif "conv16_kernel" in name or "conv_kernel" in name:  # ConvPositionEmbedding layers (conv.hip)
             cls[i] = "conv"
     return cls
 
@@ -55,6 +55,8 @@ def algorithmic(c, S=2, L=1876, d=1024, ff=2048, H=16, es=2, rb=2):
         return 4 * es * S * H * L * 64  # q, k, v read + o written
     if c in ("norm", "norm1"):
         return rows * d * (rb + es)
+    if c == "conv":  # one grouped conv layer (31 taps, 16 groups): input + output rows + weights (median of the two)
+        return rows * d * (es + rb) + d * (d // 16) * 31 * es
     return None
 
 
