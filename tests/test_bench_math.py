@@ -56,3 +56,12 @@ def test_pmc_traffic_only_at_the_measured_shape():
     assert t and t > 0 and src.startswith("profiles/")
     t, src = bench.pmc_traffic("attention", dict(c2, S=64))
     assert t is None and "not" in src
+
+
+def test_conv_class_traffic_over_algorithmic():
+    """The conv position embedding class carries its PMC traffic and algorithmic bytes (one grouped conv
+    layer: input + output rows + the 16 groups' 31-tap weights) at the C2 shape."""
+    arch = configs.get_arch("F5TTS_v1_Base")
+    e = bench.class_entry("conv", 0.0257, 8, arch, 2, 1876, 16, 50.9, 1)
+    assert e["algorithmic_bytes"] == 2 * 1876 * 1024 * 4 + 1024 * 64 * 31 * 2
+    assert e["traffic"] and 1.0 < e["traffic_over_algorithmic"] < 10.0
