@@ -18,7 +18,7 @@
 //     (sched_group_barrier): on gfx950 only a wave's OWN vector work hides under its MFMAs.
 //   * O^T = V^T . P^T: the S^T accumulators, packed to 16 bit, ARE the B operand; V^T comes from
 //     the LDS tile with ds_read_b64_tr_b16 (hardware transpose).
-//   * K/V tiles of 64 keys by LDS-DMA (global_load_lds) into a 3-deep ring shared by all waves,
+//   * K/V tiles of 64 keys by LDS-DMA (global_load_lds) into a 4-deep ring shared by all waves,
 //     XOR-swizzled (swz128) so every fragment read is conflict-free.
 //   * q carries scale*log2(e) (QKV GEMM epilogue), so scores are in log2 units.
 //   * XCD-aware block mapping: all query blocks of a (sequence, head) share one L2.
@@ -78,7 +78,7 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn16_kernel(AttnArgs a) {
   typedef typename OP::v4 v4;
   const ProbeT probe_t = probe_enter(a.probe);
   constexpr int TILE_B = 2 * 64 * 128;  // K + V tile bytes (64 keys x 64 dh x 2 B each)
-  constexpr int NS = 3;                 // LDS ring: one tile read while two are in flight
+  constexpr int NS = 4;                 // LDS ring: one tile read while three are in flight
   constexpr int CPW = 512 / (64 * NW);  // 16-B chunks of one K (or V) tile per lane
   constexpr float THR = 8.f;
   static_assert(CPW * 64 * NW == 512, "whole DMA rounds");
@@ -165,10 +165,13 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn16_kernel(AttnArgs a) {
 
   dma(0, 0);
   if (ntile > 1) dma(1, 1);
+  if (ntile > 2) dma(2, 2);
   for (int kt = 0; kt < ntile; ++kt) {
     // tile kt landed for this wave's own DMA (tile kt+1 may stay in flight); the barrier
-    // publishes every wave's part of it and retires all reads of slot (kt+2)%3 (= tile kt-1).
-    if (kt + 1 < ntile)
+    // publishes every wave's part of it and retires all reads of slot (kt+3)%4 (= tile kt-1).
+    if (kt + 2 < ntile)
+      asm volatile("s_waitcnt vmcnt(%0)" ::"i"(4 * CPW) : "memory");
+    else if (kt + 1 < ntile)
       asm volatile("s_waitcnt vmcnt(%0)" ::"i"(2 * CPW) : "memory");
     else
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -182,7 +185,7 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn16_kernel(AttnArgs a) {
       kf[0][ks] = lds_b128<0>(kaddr[ks] + so);
       kf[1][ks] = lds_b128<4096>(kaddr[ks] + so);
     });
-    if (kt + 2 < ntile) dma((kt + 2) % NS, kt + 2);
+    if (kt + 3 < ntile) dma((kt + 3) % NS, kt + 3);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 #pragma unroll
     for (int t = 0; t < 2; ++t)
