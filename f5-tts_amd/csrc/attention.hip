@@ -98,22 +98,6 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn16_kernel(AttnArgs a) {
   const int ntile = (klen + 63) / 64;
 
   const int qrow = qb * (32 * NW) + wid * 32 + (lane & 31);
-  v8 qf[4];
-#pragma unroll
-  for (int ks = 0; ks < 4; ++ks) {
-    // rows past L are clamped (their outputs are never stored)
-    uint4 v = *reinterpret_cast<const uint4*>(Q + (int64_t)min(qrow, L - 1) * 64 + ks * 16 + h * 8);
-    qf[ks] = __builtin_bit_cast(v8, v);
-    if constexpr (!PRESCALED) {  // scores in log2 units: fold scale*log2(e) into q
-      const float c = a.scale * 1.4426950408889634f;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) qf[ks][j] = from_f32<T>(to_f32(qf[ks][j]) * c);
-    }
-  }
-  // consume Q here: otherwise hipcc waits vmcnt(0) at its first use inside the tile loop, which
-  // would also drain the LDS-DMA in flight
-#pragma unroll
-  for (int ks = 0; ks < 4; ++ks) asm volatile("" ::"v"(qf[ks]));
 
   // ---- LDS-DMA of a K/V tile: chunk p = (r*NW + w)*64 + lane of the 64-row x 8-chunk image
   int dsrc[CPW];
@@ -163,9 +147,35 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn16_kernel(AttnArgs a) {
     minit[r] = 0.f;
   }
 
+  // Tile 0's K/V, then Q, then tiles 1 and 2: one counted wait covers tile 0 and Q together (in
+  // order), so Q's latency overlaps tile 0's instead of preceding it. Q is loaded by inline asm (hipcc
+  // would wait vmcnt(0), draining tiles 1 and 2, before its first use) and released by the wait below.
+  // Tiles 1 and 2 are issued even past the end of short rows (clamped rows into unused ring slots; the
+  // last tile's vmcnt(0) drains them) so that the count of loads behind Q is fixed.
   dma(0, 0);
-  if (ntile > 1) dma(1, 1);
-  if (ntile > 2) dma(2, 2);
+  u32x4 q0, q1, q2, q3;
+  {
+    // rows past L are clamped (their outputs are never stored)
+    const T* qp = Q + (int64_t)min(qrow, L - 1) * 64 + h * 8;
+    asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(q0) : "v"(qp) : "memory");
+    asm volatile("global_load_dwordx4 %0, %1, off offset:32" : "=v"(q1) : "v"(qp) : "memory");
+    asm volatile("global_load_dwordx4 %0, %1, off offset:64" : "=v"(q2) : "v"(qp) : "memory");
+    asm volatile("global_load_dwordx4 %0, %1, off offset:96" : "=v"(q3) : "v"(qp) : "memory");
+  }
+  dma(1, 1);
+  dma(2, 2);
+  asm volatile("s_waitcnt vmcnt(%4)" : "+v"(q0), "+v"(q1), "+v"(q2), "+v"(q3) : "i"(4 * CPW) : "memory");
+  const u32x4 qv[4] = {q0, q1, q2, q3};
+  v8 qf[4];
+#pragma unroll
+  for (int ks = 0; ks < 4; ++ks) {
+    qf[ks] = __builtin_bit_cast(v8, qv[ks]);
+    if constexpr (!PRESCALED) {  // scores in log2 units: fold scale*log2(e) into q
+      const float c = a.scale * 1.4426950408889634f;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) qf[ks][j] = from_f32<T>(to_f32(qf[ks][j]) * c);
+    }
+  }
   for (int kt = 0; kt < ntile; ++kt) {
     // tile kt landed for this wave's own DMA (tile kt+1 may stay in flight); the barrier
     // publishes every wave's part of it and retires all reads of slot (kt+3)%4 (= tile kt-1).
@@ -307,6 +317,7 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn16_kernel(AttnArgs a) {
     });
     mma_chunk(std::integral_constant<int, 3>{});
   }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no LDS-DMA outlives the loop (ntile == 0 included)
   probe_mark(a.probe, probe_t, 2);
   float l_tot = lrow.x + lrow.y;
   l_tot += xor32(l_tot);  // lanes l and l + 32 hold the two key halves of one query
