@@ -1,8 +1,8 @@
 #!/bin/bash
-# Round 3 final artifacts at HEAD on one box (VALU row sums, 4-slot attention ring, one packed CFG chain): smoke, default bench line (CPU baseline, +Vocos), C2 fp16, C3 / C4
+# Round 3 final artifacts at HEAD on one box (VALU row sums, 4-slot attention ring, Q between the first K/V tiles, one packed CFG chain): smoke, default bench line (CPU baseline, +Vocos), C2 fp16, C3 / C4
 # (per rank) / C5 bench lines, kernel trace of C2 calls, graph-mode PMC classes.
 set -o pipefail
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"; O=gpurun_out/r03f2; mkdir -p $O; export TMPDIR=/tmp
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"; O=gpurun_out/r03f3; mkdir -p $O; export TMPDIR=/tmp
 timeout -k 10 900 python -u -m pytest tests -m gpu -q -rf --timeout 300 --timeout-method thread > $O/gputest.log 2>&1; echo "tests rc=$?"; grep -E "passed|failed" $O/gputest.log | tail -3
 timeout -k 10 240 python __graft_entry__.py smoke > $O/smoke.log 2>&1 && echo "smoke ok" \
 && timeout -k 10 400 python bench.py > $O/bench_c2.log 2>&1 && echo "c2 ok" \
