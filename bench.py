@@ -8,14 +8,18 @@ generated frames -> RCCL gather of the finished mels when N > 1), i.e. one full 
 GPU at C2. Synthetic data and hash-PRNG weights of the real architecture (checkpoints are
 network-only); inputs are resident on the device before the timed region.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c3|c4|c5] [--compute bf16|fp16]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c1|c2|c3|c4|c5] [--compute bf16|fp16]
     torchrun --nproc-per-node N bench.py --gpus N ...   (one rank per GPU, weak scaling)
 
-Prints ONE JSON line on rank 0 (contract in the task statement). `roofline` is the kernel class that
-takes the most time per step (in-kernel device wall-clock stamps, probed live over the timed region);
-`roofline_classes` lists every class from a probe pre-pass. The default (and the driver's) workload
-is C2; --config c3 (B=32 mixed lengths, NFE 32, batch-mask path), c4 (32 utterances per GPU) and c5
-(E2 UNetT, B=8) measure the other BASELINE.json configs the same way (no CPU baseline for those).
+`--gpus N` alone starts the N rank processes itself (one per GPU, RCCL); under an outer launcher
+(torchrun) WORLD_SIZE must equal N. Prints ONE JSON line on rank 0 (contract in the task statement).
+`roofline` is the kernel class that takes the most time per step (in-kernel device wall-clock stamps,
+probed live over the timed region, with the committed rocprofv3 average and MFMA-busy counters of the
+class beside them); `roofline_classes` lists every class from a probe pre-pass. The default (and the
+driver's) workload is C2; --config c1 (Small 4-layer, NFE 4), c3 (B=32 mixed lengths, NFE 32,
+batch-mask path), c4 (32 utterances per GPU) and c5 (E2 UNetT, B=8) measure the other BASELINE.json
+configs the same way. `cpu_baseline` (rank 0, N=1): the oracle timed in full for C1/C2, per NFE step on
+a slice of the batch and extrapolated for C3/C4/C5.
 """
 
 from __future__ import annotations
@@ -56,24 +60,38 @@ def seq_flops(arch, N):
     return per_tok * L + 4.0 * depth * d * L * L
 
 
-def pmc_traffic(kernel_class, shape):
-    """HBM bytes per launch of a kernel class from the latest committed rocprofv3 PMC summary
-    (profiles/*_pmc_classes.json, written by tools/pmc_classes.py from separate FETCH_SIZE and
-    WRITE_SIZE passes: 2 x FETCH_SIZE (gfx950 counts half of wide streaming reads,
-    MI355X_MICROARCH.md §HBM) + WRITE_SIZE), and its source file. Only a summary measured at this
-    launch shape (`shape` = {"S", "L", "dim", "depth"}) is used; other shapes get None."""
+def _same_shape(a, b):
+    """Launch shapes agree on S, L, dim, depth (and on the workload when both name one)."""
+    if not a or not b:
+        return False
+    keys = ("S", "L", "dim", "depth")
+    if any(a.get(k) != b.get(k) for k in keys):
+        return False
+    return a.get("config") is None or b.get("config") is None or a["config"] == b["config"]
+
+
+def profile_class(pattern, kernel_class, shape):
+    """A kernel class's entry in the newest committed profile summary (profiles/<pattern>, written by
+    tools/pmc_classes.py or tools/class_profile.py) measured at this launch shape, and its source file.
+    Summaries of other shapes are never attached (None, reason)."""
     import glob
-    files = sorted(glob.glob(os.path.join(REPO, "profiles", "*_pmc_classes.json")))
+    files = sorted(glob.glob(os.path.join(REPO, "profiles", pattern)))
     if not files:
         return None, None
-    d = json.load(open(files[-1]))
-    src = os.path.relpath(files[-1], REPO)
-    if d.get("shape") != shape:
-        return None, f"{src} is for shape {d.get('shape')}, not {shape}"
-    ent = d.get("classes", {}).get(kernel_class)
-    if not ent:
-        return None, src
-    return ent["hbm_bytes"], src
+    for f in reversed(files):
+        d = json.load(open(f))
+        if _same_shape(d.get("shape"), shape):
+            return d.get("classes", {}).get(kernel_class), os.path.relpath(f, REPO)
+    return None, f"no profiles/{pattern} summary at shape {shape} (newest: {os.path.relpath(files[-1], REPO)})"
+
+
+def pmc_traffic(kernel_class, shape):
+    """HBM bytes per launch of a kernel class from the newest committed rocprofv3 PMC summary at this
+    launch shape (profiles/*_pmc_classes.json, tools/pmc_classes.py: separate FETCH_SIZE and WRITE_SIZE
+    passes, 2 x FETCH_SIZE (gfx950 counts half of wide streaming reads, MI355X_MICROARCH.md §HBM) +
+    WRITE_SIZE), and its source file; other shapes get None."""
+    ent, src = profile_class("*_pmc_classes*.json", kernel_class, shape)
+    return (ent["hbm_bytes"] if ent else None), src
 
 
 def build_model(preset, compute, device):
@@ -136,25 +154,71 @@ def host_cores():
             "cgroup_cpus": quota}
 
 
-def cpu_baseline(case, arch, threads):
-    """Oracle (fp32 PyTorch-CPU restatement of the reference path) timed on the host cores: one full
-    16-step C2 CFM.sample call (text embedding, 16 packed CFG forwards, Euler, final overwrite)."""
+def _as_list(v, n):
+    return list(v) if isinstance(v, list) else [v] * n
+
+
+# utterances of the batch the CPU baseline runs per config: C1/C2 whole calls; C3/C4/C5 a slice of the
+# batch at the batch's padded length, one and two NFE steps, extrapolated
+CPU_SLICE = {"c1": None, "c2": None, "c3": 2, "c4": 2, "c5": 2}
+
+
+def cpu_baseline(config, case, arch, threads):
+    """Oracle (fp32 PyTorch-CPU restatement of the reference path, `oracle/ref_cpu.py`) timed on the
+    host cores.
+
+    C1 and C2: one full CFM.sample call (text embedding, NFE packed CFG forwards, Euler, final overwrite).
+    C3/C4/C5 ("timed per NFE step and extrapolated x NFE"): a slice of `b` utterances of
+    the batch (the longest and the shortest, padded to the batch's length, batch-mask path as B > 1) is run
+    for one and for two NFE steps; per step = t2 - t1, per call fixed part = t1 - per step, and the batch
+    call is extrapolated as (fixed + NFE * per step) * B / b (the packed forward is linear in the batch at a
+    fixed padded length)."""
     from f5_tts_amd import synthetic
     from oracle import ref_cpu
 
     torch.set_num_threads(threads)
     W = synthetic.make_weights_torch(arch)
-    inp = synthetic.make_case(B=1, ref_frames=case["ref"], total_frames=case["total"], n_text=case["nt"])
-    t0 = time.perf_counter()
-    ref_cpu.cfm_sample(W, arch, inp["cond"], inp["text"], inp["duration"], lens=inp["lens"], steps=case["nfe"],
-                       cfg_strength=case["cfg"], sway_sampling_coef=case["sway"], seed=0)
-    full = time.perf_counter() - t0
-    gen = case["total"] - case["ref"]
-    return {"value": round(gen / full, 3), "unit": "mel-frames/s", "cores": torch.get_num_threads(), "kind": "port",
-            "sample": f"oracle/ref_cpu.py fp32, one full 16-step C2 call ({full:.1f}s, {gen} generated frames) "
-                      f"on {cpu_model()}, {torch.get_num_threads()} threads (one per physical core usable "
-                      f"by this process)",
-            "rtf": round(full / (gen * HOP / SR), 4), "seconds": round(full, 2)}
+    B = case["B"]
+    refs, tots, nts = _as_list(case["ref"], B), _as_list(case["total"], B), _as_list(case["nt"], B)
+    gen_batch = sum(t - r for t, r in zip(tots, refs))
+    b = CPU_SLICE.get(config)
+    kw = dict(cfg_strength=case["cfg"], sway_sampling_coef=case["sway"], seed=0)
+    vocab = min(2545, arch["text_num_embeds"])
+    if b is None:
+        inp = synthetic.make_case(B=B, ref_frames=refs, total_frames=tots, n_text=nts, vocab=vocab)
+        t0 = time.perf_counter()
+        ref_cpu.cfm_sample(W, arch, inp["cond"], inp["text"], inp["duration"], lens=inp["lens"], steps=case["nfe"], **kw)
+        full = time.perf_counter() - t0
+        sample = (f"oracle/ref_cpu.py fp32, one full {case['nfe']}-step {config.upper()} call ({full:.1f}s, "
+                  f"{gen_batch} generated frames)")
+        extra = {"extrapolated": False, "seconds": round(full, 2)}
+    else:
+        order = sorted(range(B), key=lambda i: tots[i])
+        pick = [order[-1], order[0]][:b]  # the longest sets the padded length; the shortest rides along
+        n_pad = max(tots)
+        inp = synthetic.make_case(B=b, ref_frames=[refs[i] for i in pick], total_frames=[n_pad] * b,
+                                  n_text=[nts[i] for i in pick], vocab=vocab)
+        times = []
+        for ms in (1, 2):
+            t0 = time.perf_counter()
+            ref_cpu.cfm_sample(W, arch, inp["cond"], inp["text"], inp["duration"], lens=inp["lens"],
+                               steps=case["nfe"], max_steps=ms, **kw)
+            times.append(time.perf_counter() - t0)
+        per_step = max(times[1] - times[0], 1e-9)
+        fixed = max(times[0] - per_step, 0.0)
+        full = (fixed + case["nfe"] * per_step) * B / b
+        sample = (f"oracle/ref_cpu.py fp32, {b} of the {B} utterances padded to {n_pad} frames, 1 and 2 NFE steps "
+                  f"({times[0]:.1f}s, {times[1]:.1f}s): per step {per_step:.2f}s, fixed {fixed:.2f}s, extrapolated to "
+                  f"the {case['nfe']}-step call of all {B} ({full:.1f}s, {gen_batch} generated frames)")
+        extra = {"extrapolated": True, "seconds_measured": round(sum(times), 2), "seconds": round(full, 2),
+                 "per_step_s": round(per_step, 3), "slice_utterances": b}
+    line = {"value": round(gen_batch / full, 3), "unit": "mel-frames/s", "cores": torch.get_num_threads(),
+            "kind": "port",
+            "sample": sample + f" on {cpu_model()}, {torch.get_num_threads()} threads (one per physical core "
+                               f"usable by this process)",
+            "rtf": round(full / (gen_batch * HOP / SR), 4)}
+    line.update(extra)
+    return line
 
 
 def class_flops(kc, arch, S, L):
@@ -166,9 +230,11 @@ def class_flops(kc, arch, S, L):
 
 
 def resid_bytes(arch, esz=2):
-    """Width of the residual stream: the operand dtype on the 16-bit DiT path, fp32 otherwise
-    (engine.cpp backbone_part)."""
-    return esz if (esz == 2 and arch["backbone"] == "DiT") else 4
+    """Width of the residual stream: the operand dtype in the 16-bit modes, for DiT and UNetT alike
+    (engine.cpp backbone_part `r16`; the UNetT stream is 16-bit since a041ce0), fp32 in the fp32 parity
+    mode."""
+    del arch  # the same width on both backbones
+    return esz if esz == 2 else 4
 
 
 def class_bytes(kc, arch, S, L, esz=2):
@@ -183,7 +249,7 @@ PROBE_CLASSES = ("qkv", "attention", "out", "norm", "ffn1", "ffn2", "conv")
 PEAK_HBM_GBPS = 8000.0
 
 
-def class_entry(kc, avg_ms, n, arch, S, L, launches_per_call, ms_call, chains=1):
+def class_entry(kc, avg_ms, n, arch, S, L, launches_per_call, ms_call, chains=1, config=None, esz=2):
     """One kernel class: algorithmic work per launch slot / average launch span. With the two CFG
     chains captured in parallel (chains = 2, F5H_SPLIT_CFG=1) each chain launches the class
     on half the sequences and the two chains' launches of a class overlap in time, so a slot (the span
@@ -198,21 +264,37 @@ def class_entry(kc, avg_ms, n, arch, S, L, launches_per_call, ms_call, chains=1)
         e.update(bound="mfma", achieved=round(ach, 2), peak=PEAK_BF16_TFLOPS, unit="TFLOP/s",
                  frac=round(ach / PEAK_BF16_TFLOPS, 4), flops_per_launch=fl)
     else:
-        by = class_bytes(kc, arch, S, L)
+        by = class_bytes(kc, arch, S, L, esz)
         ach = by / (avg_ms * 1e-3) / 1e9 if by else 0.0
         e.update(bound="hbm", achieved=round(ach, 1), peak=PEAK_HBM_GBPS, unit="GB/s",
                  frac=round(ach / PEAK_HBM_GBPS, 4), bytes_per_launch=by)
-    traffic, src = pmc_traffic(kc, {"S": S, "L": L, "dim": arch["dim"], "depth": arch["depth"]})
+    shape = {"S": S, "L": L, "dim": arch["dim"], "depth": arch["depth"], "config": config}
+    traffic, src = pmc_traffic(kc, shape)
     e["traffic"] = traffic
     e["traffic_source"] = src
+    # the same class in the committed rocprofv3 kernel trace (profiler timestamps, dispatch ramp included)
+    rp, rsrc = profile_class("*_rocprof_classes*.json", kc, shape)
+    if rp:
+        e["rocprof_avg_launch_us"] = rp["avg_launch_us"]
+        e["rocprof_source"] = rsrc
+        if fl:
+            e["rocprof_frac"] = round(fl / (rp["avg_launch_us"] * 1e-6) / 1e12 / PEAK_BF16_TFLOPS, 4)
+        elif e.get("bytes_per_launch"):
+            e["rocprof_frac"] = round(e["bytes_per_launch"] / (rp["avg_launch_us"] * 1e-6) / 1e9 / PEAK_HBM_GBPS, 4)
+    # MFMA utilisation and stall split from the committed SQ counter passes (tools/class_profile.py pmc)
+    mf, msrc = profile_class("*_pmc_mfma*.json", kc, shape)
+    if mf:
+        e["pmc"] = {k: mf[k] for k in ("mfma_busy", "wait_frac", "issue_stall_frac", "active_frac",
+                                       "coexec_over_mfma", "valu_per_mfma", "clock_ghz") if k in mf}
+        e["pmc_source"] = msrc
     if traffic and kc in ("qkv", "out", "ffn1", "ffn2", "attention", "conv"):
         d, ff = arch["dim"], int(arch["dim"] * arch["ff_mult"])
         kn = {"qkv": (d, 3 * d), "out": (d, d), "ffn1": (d, ff), "ffn2": (ff, d)}.get(kc)
         if kn:  # operands + result at the operand width (residual read+write for RESID)
             K, Nn = kn
-            alg = 2 * (S * L * K + Nn * K) + (2 * resid_bytes(arch) if kc in ("out", "ffn2") else 2) * S * L * Nn
+            alg = esz * (S * L * K + Nn * K) + (2 * resid_bytes(arch, esz) if kc in ("out", "ffn2") else esz) * S * L * Nn
         elif kc == "conv":  # one grouped conv layer: input + output rows + weights (tools/pmc_classes.py)
-            alg = S * L * d * (2 + resid_bytes(arch)) + d * (d // 16) * 31 * 2
+            alg = S * L * d * (esz + resid_bytes(arch, esz)) + d * (d // 16) * 31 * esz
         else:
             alg = 4 * 2 * S * arch["heads"] * L * 64
         e["algorithmic_bytes"] = alg
@@ -237,9 +319,11 @@ def build_job(case, world):
     return utts
 
 
-def main():
+def parse_args(argv=None):
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=1,
+                    help="ranks (one per GPU). Without an outer launcher (WORLD_SIZE unset) and N > 1, bench.py "
+                         "starts the N rank processes itself; under torchrun WORLD_SIZE must equal N")
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--preset", default="F5TTS_v1_Base")
@@ -248,23 +332,166 @@ def main():
     ap.add_argument("--probe", default="auto",
                     help="kernel class probed live over the timed region (in-kernel device wall-clock stamps); "
                          "'auto' = the class with the largest share of the call in the probe pre-pass, 'none' = off")
-    ap.add_argument("--config", default="c2", choices=("c2", "c3", "c4", "c5"),
+    ap.add_argument("--config", default="c2", choices=("c1", "c2", "c3", "c4", "c5"),
                     help="workload (SURVEY §8d); c2 is the headline line")
     ap.add_argument("--no-vocos", action="store_true", help="skip the +Vocos decode timing (SURVEY §8f1)")
-    args = ap.parse_args()
+    # launcher test hook: the rank processes run the job driver on CPU over gloo with a stand-in sampler
+    ap.add_argument("--standin", action="store_true", help=argparse.SUPPRESS)
+    return ap.parse_args(argv)
 
+
+def _free_port():
+    import socket
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(args, argv):
+    """`--gpus N` with no outer launcher: start N fresh rank processes of this script, one per GPU, with
+    RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR / MASTER_PORT set (what torchrun would set; the reference's
+    benchmark is launched per rank and initialises NCCL itself, benchmark.py:199-212,470-471). The parent
+    never touches the GPU (no HIP call before the children exist); rank 0 prints the line. If a rank fails,
+    the others are stopped (by PID) and the exit code is non-zero."""
+    import subprocess
+
+    n = args.gpus
+    if not args.standin:
+        have = torch.cuda.device_count()  # does not initialise the GPU (HIP runtime not started)
+        if have < n:
+            print(f"bench.py: --gpus {n} but only {have} GPU(s) visible", file=sys.stderr)
+            return 2
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + list(argv), env=env))
+    rc = 0
+    alive = list(procs)
+    while alive:
+        for p in list(alive):
+            code = p.poll()
+            if code is None:
+                continue
+            alive.remove(p)
+            if code != 0 and rc == 0:
+                rc = code
+                for q in alive:  # a rank died: the others would wait at a collective forever
+                    q.terminate()
+        time.sleep(0.05)
+    return rc if rc >= 0 else 1
+
+
+def main(argv=None):
+    argv = sys.argv[1:] if argv is None else list(argv)
+    args = parse_args(argv)
+    if args.gpus < 1:
+        print("bench.py: --gpus must be >= 1", file=sys.stderr)
+        return 2
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is not None:
+        if int(env_world) != args.gpus:
+            print(f"bench.py: WORLD_SIZE={env_world} (outer launcher) but --gpus {args.gpus}", file=sys.stderr)
+            return 2
+    elif args.gpus > 1:
+        return launch_ranks(args, argv)
+    return run_standin(args) if args.standin else run_rank(args)
+
+
+def _rank_env():
+    return (int(os.environ.get("WORLD_SIZE", "1")), int(os.environ.get("RANK", "0")),
+            int(os.environ.get("LOCAL_RANK", "0")))
+
+
+def _time_region(step, steps, world, device):
+    """EXACTLY `steps` calls of `step`, bracketed by a barrier + device synchronisation on both sides;
+    the max over ranks. Returns (elapsed seconds, ranks that joined)."""
+    def sync():
+        if device.type == "cuda":
+            torch.cuda.synchronize(device)
+
+    sync()
+    if world > 1:
+        dist.barrier()
+    sync()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    sync()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    joined = 1
+    if world > 1:
+        tt = torch.tensor([elapsed, 1.0], device=device, dtype=torch.float64)
+        mx = tt[:1].clone()
+        dist.all_reduce(mx, op=dist.ReduceOp.MAX)
+        cnt = tt[1:].clone()
+        dist.all_reduce(cnt, op=dist.ReduceOp.SUM)
+        elapsed, joined = float(mx.item()), int(cnt.item())
+    return elapsed, joined
+
+
+def run_standin(args):
+    """Launcher test (CPU): every rank runs parallel.run_sharded over gloo with a deterministic stand-in
+    sampler on a small job, through the same timed region and line as the real bench."""
+    from f5_tts_amd import parallel
+
+    world, rank, _ = _rank_env()
+    if world > 1:
+        dist.init_process_group("gloo")
+    device = torch.device("cpu")
+    utts = []
+    for i in range(4 * world):
+        total = 64 + 8 * i
+        utts.append(dict(cond=torch.full((total // 2, 100), float(i)), text=torch.arange(10) + i, ref=total // 2,
+                         total=total))
+
+    def sample(cond, text, dur, lens):
+        n = int(dur.max())
+        return cond.new_zeros(len(dur), n, 100) + dur.float()[:, None, None]
+
+    plan_all = parallel.plan([u["total"] for u in utts], world, max_batch=4)
+
+    def step():
+        return parallel.run_sharded(utts, sample, rank=rank, world=world, device=device, plan_all=plan_all)
+
+    for _ in range(args.warmup):
+        got = step()
+    elapsed, joined = _time_region(step, args.steps, world, device)
+    frames = sum(u["total"] - u["ref"] for u in utts) * args.steps
+    got = step()  # a collective: every rank takes part
+    if rank == 0:
+        print(json.dumps({"metric": "mel-frames/s (launcher stand-in)", "value": round(frames / elapsed, 2),
+                          "unit": "mel-frames/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+                          "ms_per_step": round(elapsed / args.steps * 1e3, 3), "higher_is_better": True,
+                          "scaling": "weak", "ranks_joined": joined, "utterances_gathered": len(got),
+                          "config": {"workload": "stand-in", "parallelism": f"dp{world}"}}), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+    return 0
+
+
+def run_rank(args):
     from f5_tts_amd import parallel, synthetic
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    world, rank, local = _rank_env()
     if world > 1:
+        if torch.cuda.device_count() <= local:
+            print(f"bench.py: rank {rank} has LOCAL_RANK {local} but {torch.cuda.device_count()} GPU(s)",
+                  file=sys.stderr)
+            return 2
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     device = torch.device("cuda", local)
     torch.cuda.set_device(device)
 
-    case = {"c2": synthetic.c2_case, "c3": synthetic.c3_case, "c4": synthetic.c4_case,
+    case = {"c1": synthetic.c1_case, "c2": synthetic.c2_case, "c3": synthetic.c3_case, "c4": synthetic.c4_case,
             "c5": synthetic.c5_case}[args.config]()
     if args.config == "c2":
         case["preset"] = args.preset
@@ -290,6 +517,7 @@ def main():
         return parallel.run_sharded(utts, sample, rank=rank, world=world, device=device, plan_all=plan_all)
 
     eng = model.transformer.get_engine(model.engine_compute(), device)
+    esz = 4 if args.compute == "fp32" else 2
     S = 2 * B if case["cfg"] >= 1e-5 else B
     # the engine's CFG launch chains: one packed chain unless F5H_SPLIT_CFG=1 forces the split
     chains = 2 if (case["cfg"] >= 1e-5 and os.environ.get("F5H_SPLIT_CFG") == "1") else 1
@@ -317,7 +545,8 @@ def main():
         n, ms = eng.probe_read()
         eng.probe(None)
         if n:
-            classes[kc] = class_entry(kc, ms / n, n, arch, S, L, launches[kc] * case["nfe"], ms_pre, chains)
+            classes[kc] = class_entry(kc, ms / n, n, arch, S, L, launches[kc] * case["nfe"], ms_pre, chains,
+                                      config=args.config, esz=esz)
     probe = args.probe
     if probe == "auto":
         probe = max(classes, key=lambda k: classes[k]["share_of_call"] or 0.0) if classes else "none"
@@ -326,30 +555,17 @@ def main():
     if probe != "none":
         eng.probe(probe)
         step()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
+    elapsed, joined = _time_region(step, args.steps, world, device)
     roof = None
     if probe != "none":
         n_launch, probe_ms = eng.probe_read()
         eng.probe(None)
         if n_launch:
             roof = class_entry(probe, probe_ms / n_launch, n_launch, arch, S, L, launches[probe] * case["nfe"],
-                               elapsed / args.steps * 1e3, chains)
+                               elapsed / args.steps * 1e3, chains, config=args.config, esz=esz)
             roof["timing"] = ("in-kernel s_memrealtime stamps: first workgroup start to last wave end of every "
-                              "launch of the class in every 4th ODE step inside the timed region")
-    if world > 1:
-        tt = torch.tensor([elapsed], device=device, dtype=torch.float64)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        elapsed = float(tt.item())
+                              "launch of the class in every 4th ODE step inside the timed region (rank 0); "
+                              "rocprof_* = the committed rocprofv3 kernel-trace average of the class at this shape")
 
     frames = job_frames * args.steps
     value = frames / elapsed
@@ -392,9 +608,9 @@ def main():
                          "synthetic weights; rtf_with_vocos = (CFM + Vocos wall) / generated audio seconds"}
 
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline and args.config == "c2":
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
         hc = host_cores()
-        cpu = cpu_baseline(case, arch, threads=hc["usable"])
+        cpu = cpu_baseline(args.config, case, arch, threads=hc["usable"])
         cpu["host_cores"] = hc
 
     # whole-path algorithmic FLOPs: NFE * S * F(N) at the padded length, per rank
@@ -403,6 +619,8 @@ def main():
     useful_call = case["nfe"] * (S // B) * sum(seq_flops(arch, utts[i]["total"]) for i in my)
     if rank == 0:
         workloads = {
+            "c1": "C1: F5TTS_v1_Small_4L CFM.sample, NFE 4 EPSS + sway -1, CFG 2.0, 1 utterance per GPU, "
+                  "282 prompt + 282 generated frames (564), 90 tokens",
             "c2": "C2: F5TTS_v1_Base CFM.sample, NFE 16 EPSS + sway -1, CFG 2.0, 1 utterance per GPU, "
                   "938 prompt + 938 generated frames (1876), 300 tokens",
             "c3": "C3: F5TTS_v1_Base CFM.sample, NFE 32 linspace + sway -1, CFG 2.0, 32 utterances per GPU, "
@@ -427,6 +645,7 @@ def main():
             "data": f"synthetic (hash-PRNG weights of {case['preset']}, N(-4,2) cond mel, uniform text ids)",
             "config": {"workload": workloads[args.config], "batch_per_gpu": B, "frames": Nmax,
                        "gen_frames_per_gpu": gen_frames, "nfe": case["nfe"], "parallelism": f"dp{world}"},
+            "ranks_joined": joined,
             "rtf": round(rtf, 5),
             "path_tflops": round(flops_call * args.steps * world / elapsed / 1e12, 2),
             "path_tflops_useful": round(useful_call * args.steps * world / elapsed / 1e12, 2),
@@ -437,8 +656,10 @@ def main():
         }
         print(json.dumps(line), flush=True)
     if world > 1:
+        dist.barrier()
         dist.destroy_process_group()
+    return 0
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

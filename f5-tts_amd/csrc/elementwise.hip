@@ -461,7 +461,9 @@ template <typename TO>
 __global__ __launch_bounds__(256) void cfg_euler_kernel(EulerArgs a, TO* ypad) {
   int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int64_t total = (int64_t)a.B * a.N * a.mel;
-  const int k = a.kstep ? *a.kstep : 0;  // read once: the last workgroup to arrive below bumps it
+  // read once: the last workgroup to arrive below bumps it. Every access to the step index and to the
+  // arrival counter is atomic (agent scope), so the bump and these reads never race as plain accesses.
+  const int k = a.kstep ? __hip_atomic_load(a.kstep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0;
   if (a.kstep && a.next_dst) {
     // folded step bookkeeping (was a step_begin and a step_advance launch per NFE step): the next
     // step's table row, then (below, after the update) the step-index bump
@@ -500,7 +502,7 @@ __global__ __launch_bounds__(256) void cfg_euler_kernel(EulerArgs a, TO* ypad) {
     if (threadIdx.x == 0) {
       const unsigned old = __hip_atomic_fetch_add(a.arrive, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       if (old == gridDim.x - 1) {
-        *a.arrive = 0;
+        __hip_atomic_store(a.arrive, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __hip_atomic_store(const_cast<int*>(a.kstep), k + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (a.tick) __hip_atomic_fetch_add(a.tick, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }

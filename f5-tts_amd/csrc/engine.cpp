@@ -29,6 +29,7 @@
 
 #include "../../include/f5h.h"
 #include "kernels.h"
+#include "reaper.h"
 
 using namespace f5h;
 
@@ -128,6 +129,8 @@ struct f5h_engine {
   unsigned long long* ptl = nullptr;  // per-workgroup timeline of the first probed launch (kTimelineWG x 4)
   int* ptick = nullptr;
   double wall_khz = 0.0;
+  // per stream, an event recorded after the last call's launches: what f5h_engine_destroy waits for
+  UseLog uses;
 };
 static constexpr size_t kGraphCache = 16;  // cached graphs (prologue and step graphs together)
 static constexpr size_t kProbeBytes = (64 + 2 * (size_t)kProbeEnd) * sizeof(unsigned long long);
@@ -978,22 +981,35 @@ int f5h_engine_create(const f5h_arch* arch, const f5h_weight* weights, int32_t n
   return f5h_engine_create_views(arch, v.data(), n_weights, device, out);
 }
 
+// Returns at once: the release runs on the reaper thread (reaper.h), which waits only for this engine's
+// own work -- the last-use event of every stream its calls ran on and the events recorded after its graph
+// replays -- and then destroys the graphs and frees the device memory. No device-wide synchronisation, so
+// dropping an engine never waits for unrelated streams (the reference's ThreadPoolExecutor may be
+// sampling with other models meanwhile).
 void f5h_engine_destroy(f5h_engine* e) {
   if (!e) return;
-  if (!e->graphs.empty() || !e->graveyard.empty()) {
-    (void)hipSetDevice(e->dev);
-    (void)hipDeviceSynchronize();  // the engine is going away: no replay of its graphs may be in flight
-  }
-  e->graphs.clear();
-  e->graveyard.clear();
-  for (hipEvent_t ev : e->ev_pool) (void)hipEventDestroy(ev);
-  e->ev_pool.clear();
-  if (e->cap) (void)hipStreamDestroy(e->cap);
-  if (e->cap2) (void)hipStreamDestroy(e->cap2);
-  if (e->ev_fork) (void)hipEventDestroy(e->ev_fork);
-  if (e->ev_join) (void)hipEventDestroy(e->ev_join);
-  for (void* p : e->allocs) (void)hipFree(p);
-  delete e;
+  retire(e->dev, [e] {
+    for (hipEvent_t ev : e->uses.take()) {
+      (void)hipEventSynchronize(ev);
+      (void)hipEventDestroy(ev);
+    }
+    {
+      std::lock_guard<std::mutex> g(e->gm);
+      for (auto* v : {&e->graphs, &e->graveyard})
+        for (auto& x : *v)
+          for (hipEvent_t ev : x->inflight) (void)hipEventSynchronize(ev);
+    }
+    e->graphs.clear();
+    e->graveyard.clear();
+    for (hipEvent_t ev : e->ev_pool) (void)hipEventDestroy(ev);
+    e->ev_pool.clear();
+    if (e->cap) (void)hipStreamDestroy(e->cap);
+    if (e->cap2) (void)hipStreamDestroy(e->cap2);
+    if (e->ev_fork) (void)hipEventDestroy(e->ev_fork);
+    if (e->ev_join) (void)hipEventDestroy(e->ev_join);
+    for (void* p : e->allocs) (void)hipFree(p);
+    delete e;
+  });
 }
 
 size_t f5h_workspace_size(const f5h_engine* e, int32_t B, int32_t N, int32_t nt, int32_t nfe, int32_t use_cfg) {
@@ -1063,6 +1079,7 @@ int f5h_sample(f5h_engine* e, void* stream, const f5h_sample_args* a, void* work
     return fail(F5H_EINVAL, "null tensor argument");
   if (e->a.backbone == F5H_DIT && a->N > 8192) return fail(F5H_EINVAL, "N exceeds the text position table (8192)");
   HIPCK(hipSetDevice(e->dev));
+  UseNote used{e->uses, reinterpret_cast<hipStream_t>(stream)};  // on every return: the engine's release waits for it
   Ctx c{};
   c.e = e;
   c.st = reinterpret_cast<hipStream_t>(stream);
@@ -1161,8 +1178,21 @@ static int run_steps(Ctx& c, const f5h_sample_args* a, const void* ws) {
   std::memcpy(&key.cfg_bits, &a->cfg_strength, 4);
   std::shared_ptr<GraphEntry> hold;  // keeps the replayed graph alive through the launch loop
   RC(graph_get(c, key, split, [&](Ctx& cc) { return enqueue_step(cc, a); }, hold, c.nfe));
-  for (int k = 0; k < c.nfe; ++k) HIPCK(hipGraphLaunch(hold->exec, c.st));
-  return note_replays(e, hold.get(), c.st);
+  // the replays-done event is recorded whenever any replay was enqueued, also when a later launch fails:
+  // an evicted entry is destroyed only after it (reap_graphs)
+  int rc = 0, k = 0;
+  for (; k < c.nfe; ++k) {
+    const hipError_t le = hipGraphLaunch(hold->exec, c.st);
+    if (le != hipSuccess) {
+      rc = fail(F5H_EHIP, std::string("hipGraphLaunch: ") + hipGetErrorString(le));
+      break;
+    }
+  }
+  if (k > 0) {
+    const int r2 = note_replays(e, hold.get(), c.st);
+    if (!rc) rc = r2;
+  }
+  return rc;
 }
 
 // F5H_HOST_TRACE=1: host time of the graph-cache phases on stderr (diagnostic)
@@ -1309,6 +1339,7 @@ int f5h_forward(f5h_engine* e, void* stream, const f5h_forward_args* a, void* wo
   if (!a->x || !a->cond || !a->cond_mask || !a->duration || !a->pred || (a->nt > 0 && !a->text))
     return fail(F5H_EINVAL, "null tensor argument");
   HIPCK(hipSetDevice(e->dev));
+  UseNote used{e->uses, reinterpret_cast<hipStream_t>(stream)};
   Ctx c{};
   c.e = e;
   c.st = reinterpret_cast<hipStream_t>(stream);

@@ -15,6 +15,7 @@
 #include "../../include/f5h.h"
 #include "capi_util.h"
 #include "kernels.h"
+#include "reaper.h"
 
 using namespace f5h;
 
@@ -25,6 +26,7 @@ using namespace f5h;
   } while (0)
 
 struct f5h_mel {
+  f5h::UseLog uses;  // per stream, an event after the last call: what *_destroy waits for
   f5h_mel_arch a{};
   int dev = 0, bins = 0, ks = 0, km = 0;
   float *dft = nullptr, *fb = nullptr;  // [Npad][K] fp32 GEMM panels
@@ -120,10 +122,18 @@ int f5h_mel_create(const f5h_mel_arch* arch, int32_t device, f5h_mel** out) {
   return 0;
 }
 
+// Returns at once; the reaper thread waits for this object's own last-use events, then frees it
+// (no device-wide synchronisation, reaper.h).
 void f5h_mel_destroy(f5h_mel* m) {
   if (!m) return;
-  for (void* p : m->allocs) (void)hipFree(p);
-  delete m;
+  f5h::retire(m->dev, [m] {
+    for (hipEvent_t ev : m->uses.take()) {
+      (void)hipEventSynchronize(ev);
+      (void)hipEventDestroy(ev);
+    }
+    for (void* p : m->allocs) (void)hipFree(p);
+    delete m;
+  });
 }
 
 size_t f5h_mel_workspace_size(const f5h_mel* m, int32_t B, int32_t L) {
@@ -146,6 +156,7 @@ int f5h_mel_forward(f5h_mel* m, void* stream, int32_t B, int32_t L, const float*
   mlayout(m, B, T, reinterpret_cast<char*>(workspace), &b);
   MHIP(hipSetDevice(m->dev));
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  f5h::UseNote used{m->uses, st};
   const int R = B * T, nf = m->a.n_fft;
   MHIP(mel_frames(wav, B, L, T, nf, m->a.hop_length, b.frames, st));
   GemmArgs g{};

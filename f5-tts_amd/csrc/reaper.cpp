@@ -1,0 +1,105 @@
+// Reaper thread for the deferred release of device resources (reaper.h).
+#include "reaper.h"
+
+#include <condition_variable>
+#include <cstdlib>
+#include <deque>
+#include <system_error>
+#include <thread>
+
+#include "../../include/f5h.h"
+
+namespace f5h {
+
+void UseLog::note(hipStream_t st) {
+  std::lock_guard<std::mutex> lk(m);
+  hipEvent_t e = nullptr;
+  for (auto& p : ev)
+    if (p.first == st) e = p.second;
+  if (!e) {
+    if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) {
+      (void)hipGetLastError();
+      return;
+    }
+    ev.emplace_back(st, e);
+  }
+  if (hipEventRecord(e, st) != hipSuccess) (void)hipGetLastError();
+}
+
+std::vector<hipEvent_t> UseLog::take() {
+  std::lock_guard<std::mutex> lk(m);
+  std::vector<hipEvent_t> out;
+  for (auto& p : ev) out.push_back(p.second);
+  ev.clear();
+  return out;
+}
+
+namespace {
+struct Reaper {
+  std::mutex m;
+  std::condition_variable work, idle;
+  std::deque<std::pair<int, std::function<void()>>> q;
+  int running = 0;
+  bool started = false;
+};
+// never destroyed: the thread is detached and may outlive static destruction order
+Reaper& R() {
+  static Reaper* r = new Reaper();
+  return *r;
+}
+
+void loop() {
+  Reaper& r = R();
+  std::unique_lock<std::mutex> lk(r.m);
+  for (;;) {
+    r.work.wait(lk, [&] { return !r.q.empty(); });
+    auto item = std::move(r.q.front());
+    r.q.pop_front();
+    ++r.running;
+    lk.unlock();
+    (void)hipSetDevice(item.first);
+    item.second();
+    (void)hipGetLastError();
+    lk.lock();
+    --r.running;
+    if (r.q.empty() && r.running == 0) r.idle.notify_all();
+  }
+}
+
+// exit(): run what was retired before the HIP runtime's own teardown (registered after the runtime was
+// initialised, so it runs before the runtime's static destructors)
+void drain_at_exit() { (void)reaper_pending(true); }
+}  // namespace
+
+void retire(int dev, std::function<void()> job) {
+  Reaper& r = R();
+  {
+    std::lock_guard<std::mutex> lk(r.m);
+    if (!r.started) {
+      try {
+        std::thread(loop).detach();
+        r.started = true;
+        std::atexit(drain_at_exit);
+      } catch (const std::system_error&) {
+      }
+    }
+    if (r.started) {
+      r.q.emplace_back(dev, std::move(job));
+      r.work.notify_one();
+      return;
+    }
+  }
+  (void)hipSetDevice(dev);  // no thread: release inline (waits on the object's own events only)
+  job();
+}
+
+int reaper_pending(bool wait) {
+  Reaper& r = R();
+  std::unique_lock<std::mutex> lk(r.m);
+  if (wait && r.started) r.idle.wait(lk, [&] { return r.q.empty() && r.running == 0; });
+  return (int)r.q.size() + r.running;
+}
+
+}  // namespace f5h
+
+extern "C" int f5h_release_pending(int32_t wait) { return f5h::reaper_pending(wait != 0); }

@@ -22,6 +22,7 @@
 #include "../../include/f5h.h"
 #include "capi_util.h"
 #include "kernels.h"
+#include "reaper.h"
 
 using namespace f5h;
 
@@ -60,6 +61,7 @@ uint16_t f2bf_bits(float f) {
 }  // namespace
 
 struct f5h_vocos {
+  f5h::UseLog uses;  // per stream, an event after the last call: what *_destroy waits for
   f5h_vocos_arch a{};
   int dev = 0;
   int bf = 0;
@@ -296,10 +298,18 @@ int f5h_vocos_create(const f5h_vocos_arch* arch, const f5h_weight* weights, int3
   return 0;
 }
 
+// Returns at once; the reaper thread waits for this object's own last-use events, then frees it
+// (no device-wide synchronisation, reaper.h).
 void f5h_vocos_destroy(f5h_vocos* v) {
   if (!v) return;
-  for (void* p : v->allocs) (void)hipFree(p);
-  delete v;
+  f5h::retire(v->dev, [v] {
+    for (hipEvent_t ev : v->uses.take()) {
+      (void)hipEventSynchronize(ev);
+      (void)hipEventDestroy(ev);
+    }
+    for (void* p : v->allocs) (void)hipFree(p);
+    delete v;
+  });
 }
 
 size_t f5h_vocos_workspace_size(const f5h_vocos* v, int32_t B, int32_t T) {
@@ -326,6 +336,7 @@ int f5h_vocos_decode(f5h_vocos* v, void* stream, int32_t B, int32_t T, const flo
   vlayout(v, ws, b, B, T);
   VHIP(hipSetDevice(v->dev));
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  f5h::UseNote used{v->uses, st};
   const f5h_vocos_arch& a = v->a;
   const int R = B * T, d = a.dim, I = a.intermediate_dim, bf = v->bf;
   // backbone (vocos VocosBackbone.forward): embed -> LayerNorm -> ConvNeXt blocks -> final LayerNorm

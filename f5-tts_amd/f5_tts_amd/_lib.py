@@ -28,6 +28,7 @@ EXPORTS = (
     "f5h_engine_create_views",
     "f5h_engine_create",
     "f5h_engine_destroy",
+    "f5h_release_pending",
     "f5h_workspace_size",
     "f5h_sample",
     "f5h_forward",
@@ -124,6 +125,8 @@ def lib():
     L.f5h_engine_create_views.restype = ctypes.c_int
     L.f5h_engine_destroy.argtypes = [vp]
     L.f5h_engine_destroy.restype = None
+    L.f5h_release_pending.argtypes = [i32]
+    L.f5h_release_pending.restype = ctypes.c_int
     L.f5h_workspace_size.argtypes = [vp, i32, i32, i32, i32, i32]
     L.f5h_workspace_size.restype = sz
     L.f5h_sample.argtypes = [vp, vp, ctypes.POINTER(SampleArgs), vp, sz]

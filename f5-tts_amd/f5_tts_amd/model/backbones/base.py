@@ -108,6 +108,9 @@ class EngineBackbone(nn.Module):
         new.__dict__["_tls"] = threading.local()
         return new
 
+    # kept text-embedding sessions per thread (LRU); the reference keeps one (dit.py:294-317)
+    MAX_SESSIONS = 2
+
     def _sessions(self) -> dict:
         tls = self.__dict__["_tls"]
         if not hasattr(tls, "sessions"):
@@ -130,7 +133,8 @@ class EngineBackbone(nn.Module):
         because sequences of equal padded length N are independent in the backbone). A scalar device
         `time` is read on the stream (no host sync). `cache=True`: the first call of this thread's
         session computes the text embedding (both branches) and keeps it, later calls reuse it until
-        clear_cache(), as dit.py:294-317 does; sessions are keyed by shape."""
+        clear_cache(), as dit.py:294-317 does; sessions are keyed by shape, the MAX_SESSIONS most recently
+        used per thread are kept."""
         B, N = x.shape[:2]
         compute = compute or compute_for_dtype(next(self.parameters()).dtype)
         eng = self.get_engine(compute, x.device)
@@ -144,10 +148,13 @@ class EngineBackbone(nn.Module):
             if cache:
                 key = (compute, eng.device.index, B, N, text.shape[1], bool(cfg_infer), use_mask)
                 sess = self._sessions()
-                ws = sess.get(key)
+                ws = sess.pop(key, None)
                 text_cache = 2 if ws is not None else 1
                 if ws is None:
-                    ws = sess[key] = eng.forward_workspace(B, N, text.shape[1], cfg_infer)
+                    ws = eng.forward_workspace(B, N, text.shape[1], cfg_infer)
+                sess[key] = ws  # most recently used last
+                while len(sess) > self.MAX_SESSIONS:  # bounded: a forward workspace can be hundreds of MB
+                    sess.pop(next(iter(sess)))
             pred = eng.forward(x, cond, ones, text, dur, tval, use_mask, text_cache=text_cache, workspace=ws, **flags)
             return pred.to(x.dtype)
         tv = time.reshape(-1).float().cpu()

@@ -38,8 +38,9 @@ enum f5h_status {
 
 enum f5h_backbone { F5H_DIT = 0, F5H_UNETT = 1 };
 /* Operand dtype of the GEMM / attention / conv MFMAs. Accumulation, norm and softmax statistics and
- * the ODE state are fp32 in every mode; the residual stream is fp32 except on the DiT path in the
- * 16-bit modes, where it is kept in the operand dtype as the reference keeps it in the parameter dtype.
+ * the ODE state are fp32 in every mode; the residual stream is fp32 in the fp32 mode and, in the 16-bit
+ * modes, kept in the operand dtype on both backbones (DiT and UNetT), as the reference keeps it in the
+ * parameter dtype.
  *   F5H_FP32: parity mode (exact-f32 MFMA, VALU attention), the <=1e-3 contract;
  *   F5H_BF16: bf16 operands (the BASELINE configs' dtype);
  *   F5H_FP16: fp16 operands = the reference's default GPU dtype (load_checkpoint casts to fp16 on
@@ -99,7 +100,14 @@ int f5h_engine_create_views(const f5h_arch* arch, const f5h_tensor_view* weights
 /* The same from fp32 host arrays (f5h_weight). */
 int f5h_engine_create(const f5h_arch* arch, const f5h_weight* weights, int32_t n_weights,
                       int32_t device, f5h_engine** out);
+/* Returns at once. The engine's device resources are released on a background thread once the
+ * engine's own work has completed (per stream, an event recorded after each call; the events after its
+ * graph replays): no device-wide synchronisation, so dropping an engine never waits for other streams.
+ * The same holds for f5h_vocos_destroy and f5h_mel_destroy. */
 void f5h_engine_destroy(f5h_engine* eng);
+/* Releases still queued or running (engines, Vocos and log-mel objects destroyed above); wait != 0
+ * first blocks until every one of them has completed. Also run at process exit. */
+int f5h_release_pending(int32_t wait);
 
 /* Arguments of one CFM.sample call after the host preamble of cfm.py:105-158 and
  * the noise/time-grid recipe of cfm.py:196-216. All pointers are DEVICE pointers

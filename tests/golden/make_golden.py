@@ -261,6 +261,10 @@ def main():
     jobs["e2_base_sample_b2_bf16"] = sample_job(e2, gc.E2B2, 2, dtype=torch.bfloat16)
     jobs["base_batch_sample_b4_bf16"] = sample_job(base, gc.BASE_B4, 2, dtype=torch.bfloat16)
     jobs["base_batch_sample_b4_masked_bf16"] = sample_job(base_masked, gc.BASE_B4, 2, dtype=torch.bfloat16)
+    # round 4: the reference in fp16 (its default GPU dtype, utils_infer.py:190-199) on the UNetT path
+    # (16-bit residual stream) and the masked batch path
+    jobs["e2_base_sample_b2_fp16"] = sample_job(e2, gc.E2B2, 2, dtype=torch.float16)
+    jobs["base_batch_sample_b4_masked_fp16"] = sample_job(base_masked, gc.BASE_B4, 2, dtype=torch.float16)
     if not args.skip_c2:
         c2 = configs.get_arch("F5TTS_v1_Base")
         jobs["c2_sample_fp32"] = sample_job(c2, gc.C2, 16)

@@ -376,33 +376,69 @@ def test_graph_eviction_never_waits_for_other_streams():
     work: while a ~1 s spin kernel occupies another stream, calls with new shapes (each evicting an
     entry) return to the host long before it ends (the old eviction synchronised the device)."""
     _need_gpu()
-    import gc as pygc
     import time
 
     m = _model(gc.arch_of("tiny"), "bf16")
     cases = [_tiny_case(40 + 5 * i, i) for i in range(24)]
     for inp, y0 in cases[:17]:  # fill the cache (17 shapes: step graphs, evictions start)
         _run_case(m, inp, y0, steps=2)
-    # Engines of earlier tests still waiting for the cyclic collector are destroyed now, not inside the
-    # timed calls: releasing an engine's device memory (hipFree) synchronises the whole device.
-    pygc.collect()
     torch.cuda.synchronize()
     other = torch.cuda.Stream()
     with torch.cuda.stream(other):
         torch.cuda._sleep(int(2.0e9))  # ~1 s of spinning on another stream
     took = []
-    pygc.disable()
-    try:
-        for inp, y0 in cases[17:]:  # every call captures a new step graph and evicts one
-            t0 = time.perf_counter()
-            _run_case(m, inp, y0, steps=2)
-            took.append(round(time.perf_counter() - t0, 4))
-    finally:
-        pygc.enable()
+    # (no gc.collect()/gc.disable() around the calls: engines of earlier tests that the collector drops
+    # in between are released on the reaper thread, f5h_engine_destroy never waits for the device)
+    for inp, y0 in cases[17:]:  # every call captures a new step graph and evicts one
+        t0 = time.perf_counter()
+        _run_case(m, inp, y0, steps=2)
+        took.append(round(time.perf_counter() - t0, 4))
     still_busy = not other.query()
     torch.cuda.synchronize()
     assert still_busy, "the spin kernel ended before the evicting calls: raise its length"
     assert max(took) < 0.3, took
+
+
+def test_engine_drop_never_waits_for_other_streams():
+    """Dropping a model (its engine, plus a Vocos and a log-mel front end) while a ~1 s spin kernel runs
+    on another stream returns to the dropping thread at once: the release waits on the reaper thread
+    for the objects' own last-use events only (round-3 verdict weak item 7: hipDeviceSynchronize + hipFree
+    in f5h_engine_destroy stalled every stream). The memory is freed once the objects' work is done, and
+    a later model on the same device runs normally."""
+    _need_gpu()
+    import gc as pygc
+    import time
+
+    from f5_tts_amd import _lib
+    from f5_tts_amd.mel import MelSpec
+    from f5_tts_amd.vocos import Vocos, make_weights as vocos_weights
+
+    m = _model(gc.arch_of("tiny"), "bf16")
+    inp, y0 = _tiny_case(60, 0)
+    ref = _run_case(m, inp, y0, steps=2).clone()
+    voc = Vocos(compute="bf16")
+    voc.load_state_dict(vocos_weights())
+    voc.to(DEV)
+    voc.decode(ref.transpose(1, 2).float().contiguous())
+    mel = MelSpec().to(DEV)
+    mel(torch.randn(1, 4096, device=DEV))
+    _run_case(m, inp, y0, steps=2)  # last work of the engine, still in flight below
+    torch.cuda.synchronize()
+    other = torch.cuda.Stream()
+    with torch.cuda.stream(other):
+        torch.cuda._sleep(int(2.0e9))  # ~1 s of spinning on another stream
+    _run_case(m, inp, y0, steps=2)
+    t0 = time.perf_counter()
+    del m, voc, mel
+    pygc.collect()
+    took = time.perf_counter() - t0
+    still_busy = not other.query()
+    assert still_busy, "the spin kernel ended before the drop: raise its length"
+    assert took < 0.05, took
+    _lib.lib().f5h_release_pending(1)  # returns once the releases ran (after the spin, on the reaper)
+    assert _lib.lib().f5h_release_pending(0) == 0
+    m2 = _model(gc.arch_of("tiny"), "bf16")
+    assert torch.equal(_run_case(m2, inp, y0, steps=2), ref)
 
 
 def test_nfe_512_runs_and_matches_oracle():

@@ -99,6 +99,9 @@ CASES = [
     ("e2_base_sample_b2", "e2_base_sample_b2_bf16", "bf16"),
     ("c1_sample_fp32", "c1_sample_bf16", "bf16"),
     ("c1_sample_fp32", "c1_sample_fp16", "fp16"),
+    # round 4: fp16 (the reference's default GPU dtype) on the UNetT path and the masked batch path
+    ("e2_base_sample_b2", "e2_base_sample_b2_fp16", "fp16"),
+    ("base_batch_sample_b4_masked", "base_batch_sample_b4_masked_fp16", "fp16"),
 ]
 
 
@@ -107,4 +110,6 @@ def test_within_reference_envelope(case, lo, compute):
     _need_gpu()
     e_ours, e_ref = _envelope(case, lo, compute)
     assert e_ours <= MARGIN * e_ref, (e_ours, e_ref)
-    assert e_ours <= 1.25 * MEASURED[(case, compute)], (e_ours, MEASURED[(case, compute)])
+    measured = MEASURED.get((case, compute))
+    assert measured is not None, f"record the measured e_ours={e_ours:.6g} of {case} [{compute}] in MEASURED"
+    assert e_ours <= 1.25 * measured, (e_ours, measured)
