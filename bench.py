@@ -531,13 +531,14 @@ def run_rank(args):
         step()
     torch.cuda.synchronize()
 
-    # ---- probe pre-pass: every kernel class timed by its in-kernel stamps, one call each
+    # ---- probe pre-pass: every kernel class timed by its in-kernel stamps, one call each (skipped with
+    # --probe none: plain timing runs, e.g. interleaved A/B)
     t0 = time.perf_counter()
     step()
     torch.cuda.synchronize()
     ms_pre = (time.perf_counter() - t0) * 1e3
     classes = {}
-    for kc in PROBE_CLASSES:
+    for kc in (PROBE_CLASSES if args.probe != "none" else ()):
         eng.probe(kc)
         step()  # captures the probed step graph (the probe is part of the graph key)
         step()

@@ -89,6 +89,10 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn16_kernel(AttnArgs a) {
   attn_block(qb, bh);
   const int s_idx = bh / a.H, head = bh - s_idx * a.H;
   const int L = a.L;
+  if (a.q_len && qb * (32 * NW) >= a.q_len[s_idx]) {  // dead query block (pad rows only): nothing to write
+    probe_exit(a.probe, probe_t);
+    return;
+  }
   const int64_t base = (int64_t)bh * L * 64;
   const T* Q = reinterpret_cast<const T*>(a.q) + base;
   const T* K = reinterpret_cast<const T*>(a.k) + base;
@@ -360,6 +364,10 @@ __global__ __launch_bounds__(64) void attn_f32_kernel(AttnArgs a) {
   const float* V = reinterpret_cast<const float*>(a.v) + base;
   int klen = L;
   if (a.kv_len) klen = min(klen, a.kv_len[s_idx]);
+  if (a.q_len && (int)blockIdx.x * 64 >= a.q_len[s_idx]) {  // dead query block
+    probe_exit(a.probe, probe_t);
+    return;
+  }
   const int qrow = blockIdx.x * 64 + lane;
   float q[64], o[64];
 #pragma unroll

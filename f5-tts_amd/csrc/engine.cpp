@@ -70,13 +70,13 @@ struct Layer {
 struct GraphKey {
   const void* ws;
   int kind;  // 0: one NFE step, 1: the call prologue (inputs staged into the workspace)
-  int B, N, nt, nfe, use_cfg, batch_mask, probe, split;
+  int B, N, nt, nfe, use_cfg, batch_mask, probe, split, pad_skip;
   uint64_t kernel_epoch;  // bumped whenever a forced GEMM config changes
   uint32_t cfg_bits;
   bool operator==(const GraphKey& o) const {
     return ws == o.ws && kind == o.kind && B == o.B && N == o.N && nt == o.nt && nfe == o.nfe && kernel_epoch == o.kernel_epoch &&
            use_cfg == o.use_cfg && batch_mask == o.batch_mask && probe == o.probe && cfg_bits == o.cfg_bits &&
-           split == o.split;
+           split == o.split && pad_skip == o.pad_skip;
   }
 };
 
@@ -114,6 +114,9 @@ struct f5h_engine {
   // with the round-3 kernels the split measured C2 +2.3 %, C3 +1.0 %, C5 +1.0 % per call and C4 -0.7 %
   // (profiles/r03_ab_cfg_chains.txt; in round 1 it won C5 by 4 %). Env F5H_SPLIT_CFG, f5h_set_cfg_streams.
   int split_cfg = 2;
+  // skip the dead pad-row work of the batch path (attention query blocks and out-proj row tiles of padding
+  // only): f5h_set_pad_skip, env F5H_NO_PAD_SKIP=1 at creation turns it off. Bitwise identical results.
+  int pad_skip = 1;
   uint64_t use_ctr = 0;
   int64_t n_captures = 0, n_replays = 0;
   // probe
@@ -800,6 +803,8 @@ static int backbone_part(Ctx& c, int s0, int ns, hipStream_t st) {
       at.H = H;
       at.L = c.L;
       at.kv_len = (a.attn_mask_enabled && c.batch_mask) ? b.kvlen + s0 : nullptr;
+      // pad query rows' outputs are zeroed after to_out (modules.py:551-553): their blocks are skipped
+      at.q_len = (c.batch_mask && e->pad_skip) ? b.kvlen + s0 : nullptr;
       at.scale = 0.125f;
       at.prescaled = 1;
       ProbeScope ps(e, KC_ATTN, st, &c.site, &at.probe);
@@ -810,6 +815,12 @@ static int backbone_part(Ctx& c, int s0, int ns, hipStream_t st) {
       g.resid = h_in;                      // UNetT first half: x_in + attn(.) -> the next buffer
       g.gate = ad ? ad + 2 * d : nullptr;  // gate_msa
       g.rowkeep = keep;                    // masked_fill of pad rows (modules.py:552-554)
+      // row tiles of padding only: no work at all. Only in place (h_in null): a UNetT first-half layer
+      // writes x_in + attn into the next buffer, so its pad rows must still be copied there
+      if (keep && !h_in && e->pad_skip) {
+        g.live_len = b.kvlen + s0;
+        g.live_seq = c.L;
+      }
       ProbeScope ps(e, KC_OUT, st, &c.site, &g.probe);
       KCK(gemm(bf, epi_resid, g, st));
     }
@@ -909,6 +920,7 @@ int f5h_engine_create_views(const f5h_arch* arch, const f5h_tensor_view* weights
   e->tdp = (arch->text_dim + 63) / 64 * 64;
   if (const char* gv = getenv("F5H_GRAPH")) e->graph_mode = atoi(gv) ? 1 : 0;
   if (const char* sv = getenv("F5H_SPLIT_CFG")) e->split_cfg = std::min(2, std::max(0, atoi(sv)));
+  if (const char* pv = getenv("F5H_NO_PAD_SKIP")) e->pad_skip = (*pv == '1') ? 0 : 1;
   // host views: staged once, in their own dtype, into temporaries freed after packing
   WMap W;
   std::vector<void*> staged;
@@ -1174,6 +1186,7 @@ static int run_steps(Ctx& c, const f5h_sample_args* a, const void* ws) {
   key.probe = e->probe_class;
   const bool split = e->split_cfg == 1;  // auto (2): one packed chain
   key.split = split;
+  key.pad_skip = e->pad_skip;
   key.kernel_epoch = g_kernel_epoch.load();
   std::memcpy(&key.cfg_bits, &a->cfg_strength, 4);
   std::shared_ptr<GraphEntry> hold;  // keeps the replayed graph alive through the launch loop
@@ -1386,6 +1399,7 @@ int f5h_forward(f5h_engine* e, void* stream, const f5h_forward_args* a, void* wo
     key.use_cfg = c.use_cfg;
     key.batch_mask = c.batch_mask;
     key.probe = e->probe_class;
+    key.pad_skip = e->pad_skip;
     key.kernel_epoch = g_kernel_epoch.load();
     std::shared_ptr<GraphEntry> hold;
     RC(graph_get(c, key, false, body, hold, 1));
@@ -1470,6 +1484,14 @@ int f5h_set_cfg_streams(f5h_engine* e, int32_t n) {
   if (n < 0 || n > 2) return fail(F5H_EINVAL, "cfg streams must be 0 (auto), 1 or 2");
   std::lock_guard<std::mutex> g(e->gm);
   e->split_cfg = n == 0 ? 2 : (n == 2 ? 1 : 0);
+  return 0;
+}
+
+int f5h_set_pad_skip(f5h_engine* e, int32_t enable) {
+  if (!e) return fail(F5H_EINVAL, "null engine");
+  if (enable != 0 && enable != 1) return fail(F5H_EINVAL, "pad skip must be 0 or 1");
+  std::lock_guard<std::mutex> g(e->gm);
+  e->pad_skip = enable;
   return 0;
 }
 

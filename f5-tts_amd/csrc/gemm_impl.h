@@ -122,7 +122,10 @@ using ResT = typename std::conditional<EPI == EPI_RESID16, TC, float>::type;
 // all tile configurations stay bitwise identical whatever the compiler contracts around them.
 F5H_DEV float rope_re(float a, float b, float c, float s) { return sub_nc(mul_nc(a, c), mul_nc(b, s)); }
 F5H_DEV float rope_im(float a, float b, float c, float s) { return add_nc(mul_nc(b, c), mul_nc(a, s)); }
-F5H_DEV float resid_add(float c, float gate, float x, float keep) { return add_nc(c, mul_nc(gate, mul_nc(x, keep))); }
+// gated residual update of a kept row; a masked (pad) row keeps its residual: masked_fill(~mask, 0) of the
+// sub-layer output, then x + gate * 0 (modules.py:551-554). A select, not a multiply by the mask, so that
+// the result never depends on the pad row's sub-layer output (which the pad-row skip leaves unwritten).
+F5H_DEV float resid_add(float c, float gate, float x, bool keep) { return keep ? add_nc(c, mul_nc(gate, x)) : c; }
 
 // n / d for 0 <= n < 2^24, d > 0: float quotient + one-step correction (no integer division loop)
 F5H_DEV int fdiv(int n, int d) {
@@ -130,6 +133,17 @@ F5H_DEV int fdiv(int n, int d) {
   q -= q * d > n;
   q += (q + 1) * d <= n;
   return q;
+}
+
+// Does the row tile [m0, m0 + BM) hold a live row (GemmArgs::live_len)? Wave-uniform (scalar loads).
+F5H_DEV bool tile_live(const GemmArgs& g, int m0, int BM) {
+  if (!g.live_len) return true;
+  const int last = min(m0 + BM, g.M) - 1;
+  for (int s = m0 / g.live_seq; s <= last / g.live_seq; ++s) {
+    const int r0 = s * g.live_seq;
+    if (m0 < r0 + g.live_len[s]) return true;  // the tile starts before sequence s's live rows end
+  }
+  return false;
 }
 
 // Apply the epilogue to 8 consecutive columns [col, col+8) of output row `row`.
@@ -179,7 +193,7 @@ F5H_DEV void epi8(const GemmArgs& g, int row, int col, V8 x, const V8* pre = nul
     // 16-bit residual stream: read, add in fp32 (same rounding as EPI_RESID), store rounded
     TC* C = reinterpret_cast<TC*>(g.C);
     const TC* R = reinterpret_cast<const TC*>(g.resid ? g.resid : g.C);
-    const float keep = (g.rowkeep && !g.rowkeep[row]) ? 0.f : 1.f;
+    const bool keep = !(g.rowkeep && !g.rowkeep[row]);
     const bool v16 = full && (g.ldc % 8 == 0);
     V8 c = v16 ? load8(R + off) : V8{};
     if (!v16)
@@ -220,7 +234,7 @@ F5H_DEV void epi8(const GemmArgs& g, int row, int col, V8 x, const V8* pre = nul
 #pragma unroll
       for (int e = 0; e < 8; ++e) x.v[e] = gelu_erf(x.v[e]);
     } else if constexpr (EPI == EPI_RESID) {
-      const float keep = (g.rowkeep && !g.rowkeep[row]) ? 0.f : 1.f;
+      const bool keep = !(g.rowkeep && !g.rowkeep[row]);
       const float* R = reinterpret_cast<const float*>(g.resid ? g.resid : g.C);
       V8 c = vec ? (pre ? *pre : load8(R + off)) : V8{};
       if (!vec)
@@ -436,7 +450,7 @@ F5H_DEV void epilogue_fast_t(const GemmArgs& g, const f32x4 (&acc)[MT][NT], floa
           c = pre[PREF ? i : 0][PREF ? t : 0];
         else
           c = as_v8(ri);
-        const float keep = (!masked || ri.kb) ? 1.f : 0.f;
+        const bool keep = !masked || ri.kb;
         V8 o;
 #pragma unroll
         for (int e = 0; e < 8; ++e) o.v[e] = resid_add(c.v[e], gate8.v[e], x.v[e], keep);
@@ -514,6 +528,12 @@ __global__ __launch_bounds__(64 * WGM * WGN, 2) void gemm_kernel(GemmArgs g) {
   const int nwg = gridDim.x, b = blockIdx.x, xq = nwg >> 3, xr = nwg & 7, xcd = b & 7;
   const int bid = (xcd < xr ? xcd * (xq + 1) : xr * (xq + 1) + (xcd - xr) * xq) + (b >> 3);
   const int m0 = (bid / ntn) * BM, n0 = (bid % ntn) * BN;
+  if constexpr (EPI == EPI_RESID || EPI == EPI_RESID16) {
+    if (!tile_live(g, m0, BM)) {  // every row padding: nothing to add (C2's B = 1 never passes live_len)
+      probe_exit(g.probe, probe_t);
+      return;
+    }
+  }
   const TC* A = reinterpret_cast<const TC*>(g.A);
   const TC* W = reinterpret_cast<const TC*>(g.W);
 
@@ -775,6 +795,12 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(GemmArgs g) {
   const int nwg = gridDim.x, b = blockIdx.x, xq = nwg >> 3, xr = nwg & 7, xcd = b & 7;
   const int bid = (xcd < xr ? xcd * (xq + 1) : xr * (xq + 1) + (xcd - xr) * xq) + (b >> 3);
   const int m0 = (bid / ntn) * BM, n0 = (bid % ntn) * BN;
+  if constexpr (EPI == EPI_RESID || EPI == EPI_RESID16) {
+    if (!tile_live(g, m0, BM)) {
+      probe_exit(g.probe, probe_t);
+      return;
+    }
+  }
   const TC* A = reinterpret_cast<const TC*>(g.A);
   const TC* W = reinterpret_cast<const TC*>(g.W);
 

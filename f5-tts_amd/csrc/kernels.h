@@ -61,6 +61,10 @@ struct GemmArgs {
   DevProbe probe;                  // in-kernel launch timing (null slots: off)
   const void* resid;               // EPI_RESID / EPI_RESID16 residual input (null: C)
   const void* A2; int k_split;     // A columns [k_split, K) come from A2 (same lda), e.g. cat(x, skip)
+  // EPI_RESID / EPI_RESID16 with rowkeep: the live rows of sequence s are [s*live_seq, s*live_seq +
+  // live_len[s]); a tile with no live row skips its K loop and epilogue (its rows keep the residual, as
+  // the masked rows of a computed tile do). Null: every tile is computed.
+  const int32_t* live_len; int live_seq;
 };
 
 // compute: ComputeMode (fp32 / bf16 / fp16 operands). A and W both in the operand dtype.
@@ -72,7 +76,10 @@ void gemm_force_config(int cfg);
 struct AttnArgs {
   const void* q; const void* k; const void* v; void* o;
   int S, H, L;
-  const int32_t* kv_len;  // [S] or null
+  const int32_t* kv_len;  // [S] or null: keys [kv_len[s], L) masked
+  // [S] or null: query rows [q_len[s], L) are dead (their output is masked to 0 after to_out,
+  // modules.py:551-553): query blocks wholly past q_len[s] exit at entry and leave O unwritten
+  const int32_t* q_len;
   float scale;            // 1/sqrt(64)
   int prescaled;          // q already carries scale*log2(e): scores are in log2 units
   DevProbe probe;         // in-kernel launch timing (null slots: off)

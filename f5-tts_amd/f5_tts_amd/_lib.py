@@ -38,6 +38,7 @@ EXPORTS = (
     "f5h_set_graph_mode",
     "f5h_set_cfg_streams",
     "f5h_graph_stats",
+    "f5h_set_pad_skip",
     "f5h_op_linear",
     "f5h_op_attention",
     "f5h_gemm_force_config",
@@ -146,6 +147,8 @@ def lib():
     L.f5h_set_cfg_streams.restype = ctypes.c_int
     L.f5h_graph_stats.argtypes = [vp, ctypes.POINTER(i64), ctypes.POINTER(i64), ctypes.POINTER(i32)]
     L.f5h_graph_stats.restype = ctypes.c_int
+    L.f5h_set_pad_skip.argtypes = [vp, i32]
+    L.f5h_set_pad_skip.restype = ctypes.c_int
     L.f5h_op_linear.argtypes = [vp, i32, i32, i32, i32, vp, vp, vp, vp, vp, sz]
     L.f5h_op_linear.restype = ctypes.c_int
     L.f5h_op_attention.argtypes = [vp, i32, i32, i32, i32, vp, vp, vp, vp, i32, vp, vp, sz]

@@ -121,6 +121,11 @@ class Engine:
         0: automatic (the default; currently one chain, the faster form at C2, C3 and C5)."""
         _lib.check(_lib.lib().f5h_set_cfg_streams(self._h, int(n)), "set_cfg_streams")
 
+    def set_pad_skip(self, on: bool):
+        """Skip the batch path's dead pad-row work (attention query blocks and out-proj row tiles of
+        padding only; default on). Results are bitwise identical either way."""
+        _lib.check(_lib.lib().f5h_set_pad_skip(self._h, int(bool(on))), "set_pad_skip")
+
     def graph_stats(self):
         cap, rep, n = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int32()
         _lib.check(_lib.lib().f5h_graph_stats(self._h, ctypes.byref(cap), ctypes.byref(rep), ctypes.byref(n)),

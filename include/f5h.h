@@ -203,6 +203,11 @@ int f5h_set_graph_mode(f5h_engine* eng, int32_t mode);
  * creation). Results are bitwise identical. */
 int f5h_set_cfg_streams(f5h_engine* eng, int32_t n);
 int f5h_graph_stats(f5h_engine* eng, int64_t* captures, int64_t* replays, int32_t* cached);
+/* Batch path (use_batch_mask): pad query rows' attention output is zeroed after to_out
+ * (modules.py:551-553), so attention query blocks past a sequence's length exit at entry and out-proj row
+ * tiles of padding only skip their work (the rows keep their residual, as masked rows of a computed tile
+ * do). 1 (default; env F5H_NO_PAD_SKIP=1 at creation: 0) or 0 to compute every block. Bitwise identical. */
+int f5h_set_pad_skip(f5h_engine* eng, int32_t enable);
 
 /* Op-level entry points (parity tests / microbenchmarks). Device pointers, row-major. */
 /* C[M,N] = A[M,K] . W[N,K]^T + bias  (fp32 in/out; compute = F5H_FP32 or F5H_BF16 operands) */

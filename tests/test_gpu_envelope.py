@@ -41,6 +41,9 @@ MEASURED = {
     ("e2_base_sample_b2", "bf16"): 0.010949,  # 16-bit residual stream on UNetT (0.00824 with fp32)
     ("c1_sample_fp32", "bf16"): 0.0080304,
     ("c1_sample_fp32", "fp16"): 0.0010028,
+    # round 4 (gpurun_out/r04a/envelopes.jsonl): reference fp16 errors 0.00191 and 0.1046
+    ("e2_base_sample_b2", "fp16"): 0.0013136,
+    ("base_batch_sample_b4_masked", "fp16"): 0.0023377,
 }
 
 

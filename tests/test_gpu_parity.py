@@ -404,3 +404,54 @@ def test_maximum_length_matches_oracle_and_beyond_raises():
     with pytest.raises(RuntimeError):
         m.sample(cond=inp["cond"].to(DEV), text=inp["text"].to(DEV), duration=8193, lens=inp["lens"].to(DEV),
                  keep_trajectory=False, **kw)
+
+
+def _sample_pad_skip(m, compute, inp, y0, dur, steps, on, keep_trajectory=False):
+    eng = m.transformer.get_engine(compute, torch.device(DEV))
+    eng.set_pad_skip(on)
+    try:
+        out, traj = m.sample(cond=inp["cond"].to(DEV), text=inp["text"].to(DEV), duration=dur.to(DEV),
+                             lens=inp["lens"].to(DEV), steps=steps, cfg_strength=2.0, sway_sampling_coef=-1.0,
+                             y0=y0.to(DEV), keep_trajectory=keep_trajectory)
+        torch.cuda.synchronize()
+    finally:
+        eng.set_pad_skip(True)
+    return out.clone(), (None if traj is None else traj.clone())
+
+
+@pytest.mark.parametrize("compute", ["fp32", "bf16", "fp16"])
+@pytest.mark.parametrize("name", ["base_batch_sample_b4", "base_batch_sample_b4_masked", "dit_tiny_sample_b3",
+                                  "unett_tiny_sample_b3"])
+def test_pad_row_skip_bitwise(name, compute):
+    """The batch path's dead pad-row work (attention query blocks wholly past a sequence's length and
+    out-proj row tiles of padding only, modules.py:551-553) is skipped by default; with and without the
+    skip the outputs and whole trajectories are bitwise identical: valid rows, and pad rows, whose
+    residual feeds later layers' keys/values when the attention mask is off."""
+    _need_gpu()
+    tag, spec, nfe, sway, cfg = gc.SAMPLE_CASES[name]
+    m = _model(gc.arch_of(tag), compute)
+    inp = synthetic.make_case(**spec)
+    dur = torch.maximum(torch.maximum((inp["text"] != -1).sum(-1), inp["lens"]) + 1, inp["duration"])
+    y0 = synthetic.reference_noise(dur, gc.SEED)
+    a, ta = _sample_pad_skip(m, compute, inp, y0, dur, nfe, False, keep_trajectory=True)
+    b, tb = _sample_pad_skip(m, compute, inp, y0, dur, nfe, True, keep_trajectory=True)
+    assert torch.isfinite(b).all()
+    assert torch.equal(a, b) and torch.equal(ta, tb)
+
+
+@pytest.mark.parametrize("masked", [False, True])
+def test_pad_row_skip_bitwise_at_c3_shape(masked):
+    """C3 shape (Base, B=32, 564..1876 frames padded to 1876, 35 % padding): skip on == skip off, bit for
+    bit, over the whole trajectory (3 steps: the property does not depend on NFE)."""
+    _need_gpu()
+    from f5_tts_amd import configs
+
+    m = _model(configs.get_arch("F5TTS_v1_Base", attn_mask_enabled=masked), "bf16")
+    c3 = synthetic.c3_case()
+    inp = synthetic.make_case(B=c3["B"], ref_frames=c3["ref"], total_frames=c3["total"], n_text=c3["nt"])
+    dur = torch.tensor(c3["total"])
+    y0 = synthetic.reference_noise(dur, 11)
+    a, ta = _sample_pad_skip(m, "bf16", inp, y0, dur, 3, False, keep_trajectory=True)
+    b, tb = _sample_pad_skip(m, "bf16", inp, y0, dur, 3, True, keep_trajectory=True)
+    assert torch.isfinite(b).all()
+    assert torch.equal(a, b) and torch.equal(ta, tb)

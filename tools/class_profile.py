@@ -13,16 +13,19 @@ files hold {"shape": {S, L, dim, depth}, "classes": {...}}; bench.py attaches a 
 line only at the shape it was measured on.
 
 Derived per class (median per dispatch; chip totals):
-  mfma_busy      = SQ_VALU_MFMA_BUSY_CYCLES / (1024 SIMDs x GRBM_GUI_ACTIVE / 8): the fraction of the
-                   launch's cycles the matrix pipes were busy (GRBM_GUI_ACTIVE sums the 8 XCDs' busy
-                   cycles, MI355X_MICROARCH.md 'DVFS give-back'; MFMA_BUSY counts cycles per SIMD, 32 per
-                   32x32x16 and 16 per 16x16x32 bf16 MFMA)
+  mfma_busy      = SQ_VALU_MFMA_BUSY_CYCLES / (1024 SIMDs x clock x kernel-trace duration): the fraction
+                   of the launch's cycles the matrix pipes were busy (MFMA_BUSY sums per-SIMD busy cycles:
+                   32 per 32x32x16, 16 per 16x16x32 bf16 MFMA). clock: the slope of GRBM_GUI_ACTIVE against
+                   the duration over the classes / 8 XCDs (GRBM_GUI_ACTIVE carries a fixed per-dispatch part
+                   under the profiler, so GRBM / 8 / duration "reads high on short dispatches",
+                   MI355X_MICROARCH.md 'DVFS give-back'); mfma_busy_grbm = the raw MFMA_BUSY / (1024 x
+                   GRBM / 8), a lower bound
   wait_frac      = SQ_WAIT_ANY / SQ_WAVE_CYCLES (waves parked at s_waitcnt / barrier)
   issue_stall_frac = SQ_WAIT_INST_ANY / SQ_WAVE_CYCLES (issue stalls: MFMA dependency / pipe busy)
   active_frac    = SQ_ACTIVE_INST_ANY / SQ_WAVE_CYCLES
   coexec_over_mfma = SQ_VALU_MFMA_COEXEC_CYCLES / SQ_VALU_MFMA_BUSY_CYCLES (vector work under the MFMAs)
   valu_per_mfma  = SQ_INSTS_VALU / SQ_INSTS_MFMA
-  clock_ghz      = GRBM_GUI_ACTIVE / 8 / kernel-trace duration (reads high under ~0.3 ms dispatches)
+  clock_ghz      = the fitted clock (above), one value for the run
 """
 import csv
 import json
@@ -90,13 +93,31 @@ def pmc(config, out, *paths):
             for i, (_, _, us) in enumerate(tr):
                 if i in tcls:
                     acc[tcls[i]]["_duration_us"].append(us)
+    med = {c: {k: statistics.median(v) for k, v in d.items() if v} for c, d in acc.items()}
+    # GRBM_GUI_ACTIVE per dispatch = fixed profiler part + 8 XCDs x clock x duration (it "reads high on
+    # short dispatches", MI355X_MICROARCH.md DVFS give-back): a least-squares line over the classes gives
+    # the clock the chip held under this load and the fixed part
+    pts = [(m["_duration_us"], m["GRBM_GUI_ACTIVE"]) for m in med.values()
+           if m.get("_duration_us") and m.get("GRBM_GUI_ACTIVE")]
+    fit = None
+    if len(pts) >= 3:
+        n = len(pts)
+        mx, my = sum(p[0] for p in pts) / n, sum(p[1] for p in pts) / n
+        sxx = sum((p[0] - mx) ** 2 for p in pts)
+        if sxx > 0:
+            slope = sum((p[0] - mx) * (p[1] - my) for p in pts) / sxx
+            fit = {"clock_ghz": round(slope / 8.0 / 1e3, 4), "grbm_fixed": round(my - slope * mx, 1)}
     res = {}
-    for c, d in acc.items():
-        m = {k: statistics.median(v) for k, v in d.items() if v}
+    for c, m in med.items():
         e = {k: m[k] for k in sorted(m)}
         grbm = m.get("GRBM_GUI_ACTIVE")
-        if grbm and "SQ_VALU_MFMA_BUSY_CYCLES" in m:
-            e["mfma_busy"] = round(m["SQ_VALU_MFMA_BUSY_CYCLES"] / (NSIMD * grbm / 8.0), 4)
+        if fit and m.get("_duration_us") and "SQ_VALU_MFMA_BUSY_CYCLES" in m:
+            cyc = fit["clock_ghz"] * 1e3 * m["_duration_us"]  # kernel cycles at the fitted clock
+            e["mfma_busy"] = round(m["SQ_VALU_MFMA_BUSY_CYCLES"] / (NSIMD * cyc), 4)
+        if grbm and "SQ_VALU_MFMA_BUSY_CYCLES" in m:  # the raw form, low on short dispatches
+            e["mfma_busy_grbm"] = round(m["SQ_VALU_MFMA_BUSY_CYCLES"] / (NSIMD * grbm / 8.0), 4)
+        if m.get("SQ_INSTS_MFMA"):
+            e["mfma_cycles_per_inst"] = round(m.get("SQ_VALU_MFMA_BUSY_CYCLES", 0.0) / m["SQ_INSTS_MFMA"], 2)
         wc = m.get("SQ_WAVE_CYCLES")
         if wc:
             for k, name in (("SQ_WAIT_ANY", "wait_frac"), ("SQ_WAIT_INST_ANY", "issue_stall_frac"),
@@ -107,14 +128,14 @@ def pmc(config, out, *paths):
             e["coexec_over_mfma"] = round(m["SQ_VALU_MFMA_COEXEC_CYCLES"] / m["SQ_VALU_MFMA_BUSY_CYCLES"], 4)
         if m.get("SQ_INSTS_MFMA") and "SQ_INSTS_VALU" in m:
             e["valu_per_mfma"] = round(m["SQ_INSTS_VALU"] / m["SQ_INSTS_MFMA"], 3)
-        if grbm and m.get("_duration_us"):
-            e["clock_ghz"] = round(grbm / 8.0 / (m["_duration_us"] * 1e3), 3)
+        if fit:
+            e["clock_ghz"] = fit["clock_ghz"]
         res[c] = e
     j = {"note": f"rocprofv3 --pmc passes (each within the gfx950 per-pass slots, --kernel-trace beside) over "
                  f"tools/trace_c2.py run {config} in the shipped graph mode; median per dispatch of each class; "
                  f"SQ_WAVE_CYCLES/WAIT_*/ACTIVE_* in quad-cycles, MFMA_BUSY in cycles; derived metrics in "
                  f"tools/class_profile.py",
-         "sources": list(paths), "shape": SHAPES[config], "classes": res}
+         "sources": list(paths), "shape": SHAPES[config], "grbm_fit": fit, "classes": res}
     json.dump(j, open(out, "w"), indent=1)
     print(json.dumps(j, indent=1))
 
