@@ -86,7 +86,8 @@ struct f5h_engine {
   int bf = 0;          // compute mode (f5h_compute == ComputeMode): 0 fp32, 1 bf16, 2 fp16 operands
   size_t esz = 4;      // operand element size
   int tdp = 0;         // text_dim padded to 64
-  std::vector<void*> allocs;
+  std::vector<void*> allocs;  // device memory from the stream-ordered pool (dev_alloc), freed by the reaper
+  hipStream_t mstream = nullptr;  // the engine's own stream: creation-time uploads/packing, frees at release
   Lin t1, t2, ada, in_x, in_ct, proj_out;
   float* text_table = nullptr;
   float* freqs = nullptr;
@@ -187,12 +188,21 @@ struct WMap {
   }
 };
 
+// device buffer owned by the engine (stream-ordered pool, reaper.h: its release never syncs the device)
+static int ealloc(f5h_engine* e, size_t bytes, void** out) {
+  void* p = dev_alloc(e->dev, bytes, e->mstream);
+  if (!p) return fail(F5H_EHIP, "device allocation of " + std::to_string(bytes) + " bytes");
+  e->allocs.push_back(p);
+  *out = p;
+  return 0;
+}
+
 template <typename T>
 static int upload(f5h_engine* e, const std::vector<T>& h, T** out) {
   void* p = nullptr;
-  HIPCK(hipMalloc(&p, h.size() * sizeof(T) + 16));
-  e->allocs.push_back(p);
-  HIPCK(hipMemcpy(p, h.data(), h.size() * sizeof(T), hipMemcpyHostToDevice));
+  RC(ealloc(e, h.size() * sizeof(T) + 16, &p));
+  HIPCK(hipMemcpyAsync(p, h.data(), h.size() * sizeof(T), hipMemcpyHostToDevice, e->mstream));
+  HIPCK(hipStreamSynchronize(e->mstream));  // the host vector may go away after the return
   *out = reinterpret_cast<T*>(p);
   return 0;
 }
@@ -200,9 +210,8 @@ static int upload(f5h_engine* e, const std::vector<T>& h, T** out) {
 // zeroed device buffer owned by the engine
 static int dalloc(f5h_engine* e, size_t bytes, void** out) {
   void* p = nullptr;
-  HIPCK(hipMalloc(&p, bytes + 16));
-  e->allocs.push_back(p);
-  HIPCK(hipMemset(p, 0, bytes + 16));
+  RC(ealloc(e, bytes + 16, &p));
+  HIPCK(hipMemsetAsync(p, 0, bytes + 16, e->mstream));
   *out = p;
   return 0;
 }
@@ -212,7 +221,7 @@ static int op_dt(const f5h_engine* e) { return e->bf; }
 
 // dst[r][dst_col + c] (row stride ld_dst, element type ddt) = src[r][col0 + c] (row stride ld_src)
 static int pack_rows(const WView& v, int rows, int64_t ld_src, int col0, int ncols, void* dst, int ddt,
-                     int64_t ld_dst, int dst_row0, int dst_col) {
+                     int64_t ld_dst, int dst_row0, int dst_col, hipStream_t st) {
   PackArgs pa{};
   pa.src = v.p;
   pa.src_dt = v.dt;
@@ -232,7 +241,7 @@ static int pack_rows(const WView& v, int rows, int64_t ld_src, int col0, int nco
   pa.n[1] = 1;
   pa.n[2] = rows;
   pa.n[3] = ncols;
-  HIPCK(pack_strided(pa, nullptr));
+  HIPCK(pack_strided(pa, st));
   return 0;
 }
 
@@ -252,7 +261,7 @@ static int make_lin(f5h_engine* e, const std::vector<Block>& blocks, int K, cons
   RC(dalloc(e, (size_t)L->Npad * K * e->esz, &L->w));
   int r0 = 0;
   for (const Block& b : blocks) {
-    RC(pack_rows(*b.src, b.rows, b.ld, b.col0, b.ncols, L->w, op_dt(e), K, r0, b.dst_col));
+    RC(pack_rows(*b.src, b.rows, b.ld, b.col0, b.ncols, L->w, op_dt(e), K, r0, b.dst_col, e->mstream));
     r0 += b.rows;
   }
   if (!biases.empty()) {
@@ -261,7 +270,8 @@ static int make_lin(f5h_engine* e, const std::vector<Block>& blocks, int K, cons
     L->b = reinterpret_cast<float*>(bp);
     r0 = 0;
     for (size_t i = 0; i < blocks.size(); ++i) {
-      if (i < biases.size() && biases[i]) RC(pack_rows(*biases[i], 1, 0, 0, blocks[i].rows, L->b, 0, 0, 0, r0));
+      if (i < biases.size() && biases[i])
+        RC(pack_rows(*biases[i], 1, 0, 0, blocks[i].rows, L->b, 0, 0, 0, r0, e->mstream));
       r0 += blocks[i].rows;
     }
   }
@@ -287,7 +297,7 @@ static int vec_upload(f5h_engine* e, const WMap& W, const std::string& n, int64_
   if (!v) return fail(F5H_ENOWEIGHT, *err);
   void* p;
   RC(dalloc(e, (size_t)numel * sizeof(float), &p));
-  RC(pack_rows(*v, 1, 0, 0, (int)numel, p, 0, 0, 0, 0));
+  RC(pack_rows(*v, 1, 0, 0, (int)numel, p, 0, 0, 0, 0, e->mstream));
   *out = reinterpret_cast<float*>(p);
   return 0;
 }
@@ -342,12 +352,12 @@ static int pack_all(f5h_engine* e, const WMap& W) {
     L.K = Kct;
     L.Npad = (d + 127) / 128 * 128;
     RC(dalloc(e, (size_t)L.Npad * Kct * e->esz, &L.w));
-    RC(pack_rows(*w, d, Kin, mel, mel, L.w, op_dt(e), Kct, 0, 0));
-    RC(pack_rows(*w, d, Kin, 2 * mel, td, L.w, op_dt(e), Kct, 0, 128));
+    RC(pack_rows(*w, d, Kin, mel, mel, L.w, op_dt(e), Kct, 0, 0, e->mstream));
+    RC(pack_rows(*w, d, Kin, 2 * mel, td, L.w, op_dt(e), Kct, 0, 128, e->mstream));
     void* bp;
     RC(dalloc(e, (size_t)L.Npad * sizeof(float), &bp));
     L.b = reinterpret_cast<float*>(bp);
-    RC(pack_rows(*b, 1, 0, 0, d, L.b, 0, 0, 0, 0));
+    RC(pack_rows(*b, 1, 0, 0, d, L.b, 0, 0, 0, 0, e->mstream));
   }
   // ConvPositionEmbedding: [d, d/16, 31] -> [16][31][64 out][64 in] (zero-padded to 64 channels):
   // dst (g, t, o, i) <- src ((g*cg + o)*cg + i)*31 + t
@@ -373,7 +383,7 @@ static int pack_all(f5h_engine* e, const WMap& W) {
     pa.n[1] = 31;
     pa.n[2] = cg;
     pa.n[3] = cg;
-    HIPCK(pack_strided(pa, nullptr));
+    HIPCK(pack_strided(pa, e->mstream));
     RC(vec_upload(e, W, p + "bias", d, &e->conv_b[j], &err));
   }
   // blocks
@@ -913,6 +923,10 @@ int f5h_engine_create_views(const f5h_arch* arch, const f5h_tensor_view* weights
   }
   HIPCK(hipSetDevice(device));
   f5h_engine* e = new f5h_engine();
+  if (hipStreamCreateWithFlags(&e->mstream, hipStreamNonBlocking) != hipSuccess) {
+    delete e;
+    return fail(F5H_EHIP, "engine stream");
+  }
   e->a = *arch;
   e->dev = device;
   e->bf = arch->compute;
@@ -930,13 +944,13 @@ int f5h_engine_create_views(const f5h_arch* arch, const f5h_tensor_view* weights
     const size_t bytes = (size_t)v.numel * (v.dtype == F5H_DT_F32 ? 4 : 2);
     const void* dp = v.data;
     if (!v.on_device && bytes) {
-      void* t = nullptr;
-      if (hipMalloc(&t, bytes) != hipSuccess) {
+      void* t = dev_alloc(device, bytes, e->mstream);
+      if (!t) {
         rc = fail(F5H_EHIP, "weight staging allocation");
         break;
       }
       staged.push_back(t);
-      if (hipMemcpy(t, v.data, bytes, hipMemcpyHostToDevice) != hipSuccess) {
+      if (hipMemcpyAsync(t, v.data, bytes, hipMemcpyHostToDevice, e->mstream) != hipSuccess) {
         rc = fail(F5H_EHIP, std::string("weight staging copy: ") + v.name);
         break;
       }
@@ -953,8 +967,9 @@ int f5h_engine_create_views(const f5h_arch* arch, const f5h_tensor_view* weights
     W.m[v.name] = WView{dp, v.dtype, v.numel};
   }
   if (!rc) rc = pack_all(e, W);
-  if (!rc && hipDeviceSynchronize() != hipSuccess) rc = fail(F5H_EHIP, "weight packing");
-  for (void* t : staged) (void)hipFree(t);
+  // packing ran on the engine's stream (no device-wide synchronisation)
+  if (!rc && hipStreamSynchronize(e->mstream) != hipSuccess) rc = fail(F5H_EHIP, "weight packing");
+  for (void* t : staged) dev_free(t, e->mstream);
   if (rc) {
     f5h_engine_destroy(e);
     return rc;
@@ -962,21 +977,15 @@ int f5h_engine_create_views(const f5h_arch* arch, const f5h_tensor_view* weights
   {
     void* p = nullptr;
     int khz = 0;
-    if (hipMalloc(&p, kProbeBytes) != hipSuccess || hipMemset(p, 0, kProbeBytes) != hipSuccess) {
-      if (p) (void)hipFree(p);
+    void* tl = nullptr;
+    if (dalloc(e, kProbeBytes, &p) || dalloc(e, (size_t)kTimelineWG * 4 * sizeof(unsigned long long), &tl) ||
+        hipStreamSynchronize(e->mstream) != hipSuccess) {
       f5h_engine_destroy(e);
-      return fail(F5H_EHIP, "probe stamp buffer");
+      return fail(F5H_EHIP, "probe buffers");
     }
-    e->allocs.push_back(p);
     e->pstamp = reinterpret_cast<unsigned long long*>(p);
     e->pslots = e->pstamp + 64;
     e->ptick = reinterpret_cast<int*>(e->pstamp);
-    void* tl = nullptr;
-    if (hipMalloc(&tl, (size_t)kTimelineWG * 4 * sizeof(unsigned long long)) != hipSuccess) {
-      f5h_engine_destroy(e);
-      return fail(F5H_EHIP, "probe timeline buffer");
-    }
-    e->allocs.push_back(tl);
     e->ptl = reinterpret_cast<unsigned long long*>(tl);
     if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, device) == hipSuccess) e->wall_khz = khz;
   }
@@ -1019,7 +1028,9 @@ void f5h_engine_destroy(f5h_engine* e) {
     if (e->cap2) (void)hipStreamDestroy(e->cap2);
     if (e->ev_fork) (void)hipEventDestroy(e->ev_fork);
     if (e->ev_join) (void)hipEventDestroy(e->ev_join);
-    for (void* p : e->allocs) (void)hipFree(p);
+    // stream-ordered releases into the pool: no device-wide wait (hipFree would wait for every stream)
+    for (void* p : e->allocs) dev_free(p, e->mstream);
+    if (e->mstream) (void)hipStreamDestroy(e->mstream);
     delete e;
   });
 }
@@ -1539,8 +1550,8 @@ int f5h_op_linear(void* stream, int32_t compute, int32_t M, int32_t N, int32_t K
 }
 
 int f5h_gemm_force_config(int32_t cfg) {
-  if (cfg != -1 && cfg != 0 && cfg != 1 && cfg != 5 && cfg != 11)
-    return fail(F5H_EINVAL, "gemm config must be -1, 0, 1, 5 or 11");
+  if (cfg != -1 && cfg != 0 && cfg != 1 && cfg != 5 && cfg != 11 && cfg != 12)
+    return fail(F5H_EINVAL, "gemm config must be -1, 0, 1, 5, 11 or 12");
   gemm_force_config(cfg);
   g_kernel_epoch.fetch_add(1);
   return 0;

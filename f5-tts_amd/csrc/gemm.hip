@@ -14,6 +14,15 @@ static int gemm_env_cfg() {
 }
 
 
+// The 256x256 configuration of the large batches: 11 (ping-pong) or 12 (8-phase); env F5H_LARGE_CFG.
+static int large_cfg() {
+  static const int v = [] {
+    const char* e = getenv("F5H_LARGE_CFG");
+    return (e && atoi(e) == 12) ? 12 : 11;
+  }();
+  return v;
+}
+
 // Tile choice for a bf16 GEMM among the 2-blocks-per-CU configurations 0, 1, 5: time ~
 // rounds x tile work / relative efficiency, with rounds = ceil(tiles / 512 block slots) and
 // efficiencies from tools/gemm_tune.py on MI355X (C3-sized GEMMs: 64x128 0.57, 128x128 0.74,
@@ -22,7 +31,7 @@ static int pick_cfg(const GemmArgs& a) {
   // Large batches (C3/C4/C5: thousands of 256x256 tiles, many rounds per CU): the 8-wave
   // ping-pong 256x256 kernel (cfg 11), 5-6 % faster than the best 4-wave tile there
   // (tools/gemm_tune.py: C3 QKV 856 vs 907 us, C3 FFN2 512 vs 544 us).
-  if (a.K % 64 == 0 && (int64_t)((a.M + 255) / 256) * ((a.N + 255) / 256) >= 1024) return 11;
+  if (a.K % 64 == 0 && (int64_t)((a.M + 255) / 256) * ((a.N + 255) / 256) >= 1024) return large_cfg();
   struct Opt { int cfg, bm, bn; float eff; };
   constexpr Opt opts[3] = {{5, 192, 128, 0.86f}, {1, 128, 128, 0.74f}, {0, 64, 128, 0.57f}};
   int best = 0;

@@ -339,7 +339,7 @@ F5H_DEV void epilogue_fast_t(const GemmArgs& g, const f32x4 (&acc)[MT][NT], floa
   if constexpr (EPI == EPI_QKV) {
     // a wave's 64 columns are one head of one of q/k/v (cbase % 64 == 0): wave-uniform, so the
     // destination descriptor lives in scalar registers (a per-lane one costs a waterfall loop per store)
-    static_assert(WN == 64, "one head per wave");
+    static_assert(WN <= 64 && 64 % WN == 0, "a wave's columns lie in one head");
     const int inner = g.heads * 64;
     which = __builtin_amdgcn_readfirstlane(fdiv(cbase, inner));
     const int hc = col - which * inner;
@@ -957,6 +957,247 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(GemmArgs g) {
   probe_exit(g.probe, probe_t);
 }
 
+// ======================================================================================
+// 256x256 8-phase GEMM (16-bit operands; cdna_hip_programming.md §5, "The 256² 8-phase template"):
+// 512 threads = 8 waves, one block per CU. K-tiles of 64 alternate between two 64 KB LDS buffers; a
+// buffer holds the tile's A rows [0,256) and W rows [0,256) as four 128-row halves (A-top, A-bottom,
+// B-left, B-right, 16 KB each, 128-byte rows XOR-swizzled by swz128g so every fragment read is one
+// conflict-free ds_read_b128). Each K-tile runs as 4 phases, one 128x128 quadrant (A half x B half) of
+// the block tile each; in a quadrant the 8 waves are 2 (M) x 4 (N), wave (wr, wc) computing rows
+// wr*64..+64 and columns wc*32..+32 of it (4 x 2 fragments x 2 k-slabs = 16 MFMAs 16x16x32). A phase:
+// fragment reads -> one half-tile of LDS-DMA (2 global_load_lds per thread) -> [phase 3: counted vmcnt]
+// -> s_barrier -> lgkmcnt(0) -> 16 MFMAs -> s_barrier:
+//   phase 0  (A-top, B-left):     reads A-top (8) + B-left (4)   DMA: A-bottom of tile t+1
+//   phase 1  (A-top, B-right):    reads B-right (4)              DMA: A-top    of tile t+2 (last read in phase 0)
+//   phase 2  (A-bottom, B-right): reads A-bottom (8)             DMA: B-left   of tile t+2 (last read in phase 0)
+//   phase 3  (A-bottom, B-left):  no reads (registers kept)      DMA: B-right  of tile t+2 (last read in phase 1),
+//            then vmcnt(6): tile t+1's last half (issued in phase 0) has landed, the three halves of tile
+//            t+2 stay in flight across the barrier (never vmcnt(0) in the steady state).
+// RAW: a half is read in a phase after the barrier that follows its wait. WAR: a half is restaged one phase
+// after the phase that read it (every wave retired those reads by lgkmcnt(0) before the barrier ending that
+// phase); A-bottom two phases after. Each accumulator takes its k-slabs and K-tiles in order, so the results
+// are bitwise those of the other tile configurations.
+// ======================================================================================
+template <typename TC, int EPI, bool FAST = false>
+__global__ __launch_bounds__(512, 1) void gemm_8p_kernel(GemmArgs g) {
+  const ProbeT probe_t = probe_enter(g.probe);
+  constexpr int BM = 256, BN = 256, KT = 64;
+  constexpr int HALF = 128 * 128;      // bytes of one 128-row half (128-byte rows)
+  constexpr int BUF = 4 * HALF;        // one K-tile: A-top, A-bottom, B-left, B-right
+  constexpr int QW = 32, EPAD = QW + 4;  // a wave's columns per quadrant; epilogue strip row (fp32)
+  __shared__ __attribute__((aligned(16))) uint4 lds[2 * BUF / 16];
+  typedef typename Op16<TC>::v8 v8;
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = wid >> 2, wc = wid & 3;
+  const int ntn = (g.N + BN - 1) / BN;
+  const int nwg = gridDim.x, b = blockIdx.x, xq = nwg >> 3, xr = nwg & 7, xcd = b & 7;
+  const int bid = (xcd < xr ? xcd * (xq + 1) : xr * (xq + 1) + (xcd - xr) * xq) + (b >> 3);
+  const int m0 = (bid / ntn) * BM, n0 = (bid % ntn) * BN;
+  if constexpr (EPI == EPI_RESID || EPI == EPI_RESID16) {
+    if (!tile_live(g, m0, BM)) {
+      probe_exit(g.probe, probe_t);
+      return;
+    }
+  }
+  const TC* A = reinterpret_cast<const TC*>(g.A);
+  const TC* W = reinterpret_cast<const TC*>(g.W);
+  const TC* A2 = reinterpret_cast<const TC*>(g.A2);
+
+  // ---- DMA sources: thread tid fills chunks p = j*512 + tid (j = 0, 1) of each half: row p >> 3, slot p & 7,
+  // holding the global chunk swz128g(row, slot) (an involution: the reader XORs the same way)
+  int64_t soff[4][2];
+#pragma unroll
+  for (int h = 0; h < 4; ++h)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int p = j * 512 + tid, row = p >> 3, slot = p & 7;
+      const int chunk = swz128g(row, slot);
+      if (h < 2) {
+        const int m = min(m0 + h * 128 + row, g.M - 1);  // rows past M feed only unstored outputs
+        soff[h][j] = (int64_t)m * g.lda + chunk * 8;
+      } else {
+        const int n = min(n0 + (h - 2) * 128 + row, g.N - 1);
+        soff[h][j] = (int64_t)n * g.ldw + chunk * 8;
+      }
+    }
+  char* lds_c = reinterpret_cast<char*>(lds);
+  auto dma_half = [&](int t, int h) {  // half h (0 A-top, 1 A-bottom, 2 B-left, 3 B-right) of K-tile t
+    const int k0 = t * KT;
+    char* dst = lds_c + (t & 1) * BUF + h * HALF + wid * 64 * 16;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const TC* src;
+      if (h < 2)
+        src = (A2 && k0 >= g.k_split) ? A2 + soff[h][j] + (k0 - g.k_split) : A + soff[h][j] + k0;
+      else
+        src = W + soff[h][j] + k0;
+      __builtin_amdgcn_global_load_lds((const void*)src, (LDS_PTR(void))(dst + j * 512 * 16), 16, 0, 0);
+    }
+  };
+
+  // ---- fragment read addresses: fragment rows r satisfy r & 15 == lane & 15, so the swizzled chunk of
+  // k-slab s is a lane constant; the halves and fragments sit at immediate offsets
+  const uint32_t lds0 = (uint32_t)(uintptr_t)(LDS_PTR(void))lds;
+  const int fr = lane & 15, q = lane >> 4;
+  uint32_t abase[2], bbase[2];
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+    abase[s] = lds0 + (wr * 64 + fr) * 128 + swz128g(fr, s * 4 + q) * 16;
+    bbase[s] = lds0 + 2 * HALF + (wc * 32 + fr) * 128 + swz128g(fr, s * 4 + q) * 16;
+  }
+
+  f32x4 acc[2][2][4][2];  // [A half][B half][fragment row][fragment column]
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int c = 0; c < 2; ++c)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[a][c][i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  u32x4 af[4][2], bl[2][2], br[2][2];  // A rows of one half (4 frags x 2 slabs); B-left, B-right (2 x 2)
+  auto read_a = [&](uint32_t so, auto H) {
+    constexpr int hh = decltype(H)::value;
+    static_for<0, 4>([&](auto I) {
+      constexpr int i = decltype(I)::value;
+      af[i][0] = lds_read_b128<hh * HALF + i * 16 * 128>(abase[0] + so);
+      af[i][1] = lds_read_b128<hh * HALF + i * 16 * 128>(abase[1] + so);
+    });
+  };
+  auto read_b = [&](uint32_t so, auto H, u32x4 (&bf)[2][2]) {
+    constexpr int hh = decltype(H)::value;
+    static_for<0, 2>([&](auto J) {
+      constexpr int j = decltype(J)::value;
+      bf[j][0] = lds_read_b128<hh * HALF + j * 16 * 128>(bbase[0] + so);
+      bf[j][1] = lds_read_b128<hh * HALF + j * 16 * 128>(bbase[1] + so);
+    });
+  };
+  auto fence_regs = [&]() {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      asm volatile("" : "+v"(af[i][0]));
+      asm volatile("" : "+v"(af[i][1]));
+    }
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      asm volatile("" : "+v"(bl[j][0]));
+      asm volatile("" : "+v"(bl[j][1]));
+      asm volatile("" : "+v"(br[j][0]));
+      asm volatile("" : "+v"(br[j][1]));
+    }
+  };
+  // barrier, the phase's reads retired, the quadrant's 16 MFMAs, barrier
+  auto compute = [&](auto HA, auto HB, const u32x4 (&bf)[2][2]) {
+    constexpr int ha = decltype(HA)::value, hb = decltype(HB)::value;
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    fence_regs();
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int s = 0; s < 2; ++s)
+          acc[ha][hb][i][j] = Op16<TC>::mma16(__builtin_bit_cast(v8, af[i][s]), __builtin_bit_cast(v8, bf[j][s]),
+                                              acc[ha][hb][i][j]);
+    __builtin_amdgcn_s_setprio(0);
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+  };
+  using I0 = std::integral_constant<int, 0>;
+  using I1 = std::integral_constant<int, 1>;
+
+  const int T = g.K / KT;
+  // prologue: tile 0 (all four halves), tile 1 (A-top, B-left, B-right); wait for tile 0
+  dma_half(0, 0);
+  dma_half(0, 2);
+  dma_half(0, 3);
+  dma_half(0, 1);
+  if (T > 1) {
+    dma_half(1, 0);
+    dma_half(1, 2);
+    dma_half(1, 3);
+    asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __builtin_amdgcn_s_barrier();
+  probe_mark(g.probe, probe_t, 1);
+  for (int t = 0; t < T; ++t) {
+    const uint32_t so = (uint32_t)((t & 1) * BUF);
+    const bool more1 = t + 1 < T, more2 = t + 2 < T;
+    // phase 0: (A-top, B-left)
+    read_b(so, I0{}, bl);
+    read_a(so, I0{});
+    if (more1) dma_half(t + 1, 1);
+    compute(I0{}, I0{}, bl);
+    // phase 1: (A-top, B-right)
+    read_b(so, I1{}, br);
+    if (more2) dma_half(t + 2, 0);
+    compute(I0{}, I1{}, br);
+    // phase 2: (A-bottom, B-right)
+    read_a(so, I1{});
+    if (more2) dma_half(t + 2, 2);
+    compute(I1{}, I1{}, br);
+    // phase 3: (A-bottom, B-left); tile t+1 must have landed before this phase's first barrier
+    if (more2) {
+      dma_half(t + 2, 3);
+      asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    compute(I1{}, I0{}, bl);
+  }
+  __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0) (already so), told to hipcc
+  __syncthreads();
+  probe_mark(g.probe, probe_t, 2);
+
+  // ---- epilogue per quadrant block (64 rows x 32 columns of one head for QKV), through the wave's strip
+  float* Cs = reinterpret_cast<float*>(lds) + wid * 16 * EPAD;
+  static_for<0, 4>([&](auto QB) {
+    constexpr int ha = decltype(QB)::value >> 1, hb = decltype(QB)::value & 1;
+    const int rbase = m0 + ha * 128 + wr * 64, cbase = n0 + hb * 128 + wc * QW;
+    if constexpr (FAST) {
+      const V8 none[1][1] = {};
+      epilogue_fast<TC, EPI, 4, 2, QW, EPAD, false>(g, acc[ha][hb], Cs, rbase, cbase, lane, none);
+    } else {
+      constexpr int CH = QW / 8;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) Cs[(q * 4 + r) * EPAD + j * 16 + fr] = acc[ha][hb][i][j][r];
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        for (int idx = lane; idx < 16 * CH; idx += 64) {
+          const int rr = idx / CH, cc = idx % CH;
+          const int row = rbase + i * 16 + rr, col = cbase + cc * 8;
+          const float* sp = Cs + rr * EPAD + cc * 8;
+          float4 x0 = *reinterpret_cast<const float4*>(sp), x1 = *reinterpret_cast<const float4*>(sp + 4);
+          if (row < g.M && col < g.N)
+            epi8<TC, EPI>(g, row, col, V8{{x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w}});
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      }
+    }
+  });
+  probe_exit(g.probe, probe_t);
+}
+
+template <typename TC, int EPI>
+static void launch_8p(const GemmArgs& a, hipStream_t st);
+
 // the fast epilogue: whole-column tiles, 16-B aligned rows, destinations a buffer descriptor covers
 template <int EPI>
 static bool fast_epi_ok(const GemmArgs& a, int BN) {
@@ -988,6 +1229,20 @@ static void launch_pp(const GemmArgs& a, hipStream_t st) {
 // ping-pong geometries; none won a shape, so they are no longer built — DESIGN.md §3.)
 // Per-CU LDS-DMA intake (~37 B/clk) bounds the small tiles: bytes per MFLOP staged =
 // 64*(BM+BN)/(BM*BN) KB, so 64x128 -> 24, 128x128 -> 16, 256x256 -> 8.
+template <typename TC, int EPI>
+static void launch_8p(const GemmArgs& a, hipStream_t st) {
+  const int tiles = ((a.M + 255) / 256) * ((a.N + 255) / 256);
+  constexpr bool HOT = EPI == EPI_QKV || EPI == EPI_RESID || EPI == EPI_RESID16 || EPI == EPI_GELU_TANH ||
+                       EPI == EPI_GELU_ERF_OP || EPI == EPI_STORE || EPI == EPI_STORE16 || EPI == EPI_INPROJ;
+  if constexpr (HOT) {
+    if (fast_epi_ok<EPI>(a, 256)) {
+      hipLaunchKernelGGL((gemm_8p_kernel<TC, EPI, true>), dim3(tiles), dim3(512), 0, st, a);
+      return;
+    }
+  }
+  hipLaunchKernelGGL((gemm_8p_kernel<TC, EPI>), dim3(tiles), dim3(512), 0, st, a);
+}
+
 template <typename TC, int EPI, int BM, int BN, int WGM, int WGN, int NS, int KB = 128>
 static void launch_cfg(const GemmArgs& a, hipStream_t st) {
   const int tiles = ((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN);
@@ -1015,8 +1270,11 @@ static hipError_t launch_t(const GemmArgs& a, hipStream_t st) {
     case 5: launch_cfg<TC, EPI, 192, 128, 2, 2, 2>(a, st); break;
     default:
       if constexpr (is16<TC>()) {
-        if (cfg != 11 || a.K % 64) return hipErrorInvalidValue;  // ping-pong: whole K64 phases
-        launch_pp<TC, EPI, 256, 256, 1, 4, 1, 3>(a, st);
+        if ((cfg != 11 && cfg != 12) || a.K % 64) return hipErrorInvalidValue;  // whole K64 tiles
+        if (cfg == 11)
+          launch_pp<TC, EPI, 256, 256, 1, 4, 1, 3>(a, st);
+        else
+          launch_8p<TC, EPI>(a, st);
         break;
       }
       return hipErrorInvalidValue;

@@ -32,11 +32,13 @@ struct f5h_mel {
   float *dft = nullptr, *fb = nullptr;  // [Npad][K] fp32 GEMM panels
   int dft_npad = 0, fb_npad = 0;
   std::vector<void*> allocs;
+  hipStream_t mstream = nullptr;  // uploads at creation, stream-ordered frees at release (reaper.h)
   int upload(const std::vector<float>& h, float** out) {
-    void* p = nullptr;
-    MHIP(hipMalloc(&p, h.size() * sizeof(float) + 16));
+    void* p = f5h::dev_alloc(dev, h.size() * sizeof(float) + 16, mstream);
+    if (!p) return f5h_internal_fail(F5H_EHIP, "mel device allocation");
     allocs.push_back(p);
-    MHIP(hipMemcpy(p, h.data(), h.size() * sizeof(float), hipMemcpyHostToDevice));
+    MHIP(hipMemcpyAsync(p, h.data(), h.size() * sizeof(float), hipMemcpyHostToDevice, mstream));
+    MHIP(hipStreamSynchronize(mstream));
     *out = reinterpret_cast<float*>(p);
     return 0;
   }
@@ -92,6 +94,10 @@ int f5h_mel_create(const f5h_mel_arch* arch, int32_t device, f5h_mel** out) {
   f5h_mel* m = new f5h_mel();
   m->a = a;
   m->dev = device;
+  if (hipStreamCreateWithFlags(&m->mstream, hipStreamNonBlocking) != hipSuccess) {
+    delete m;
+    return f5h_internal_fail(F5H_EHIP, "mel stream");
+  }
   m->bins = a.n_fft / 2 + 1;
   m->ks = (2 * m->bins + 63) / 64 * 64;
   m->km = (m->bins + 31) / 32 * 32;
@@ -131,7 +137,8 @@ void f5h_mel_destroy(f5h_mel* m) {
       (void)hipEventSynchronize(ev);
       (void)hipEventDestroy(ev);
     }
-    for (void* p : m->allocs) (void)hipFree(p);
+    for (void* p : m->allocs) f5h::dev_free(p, m->mstream);
+    if (m->mstream) (void)hipStreamDestroy(m->mstream);
     delete m;
   });
 }

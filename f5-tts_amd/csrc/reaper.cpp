@@ -35,6 +35,55 @@ std::vector<hipEvent_t> UseLog::take() {
 }
 
 namespace {
+std::mutex g_pool_m;
+std::vector<std::pair<int, hipMemPool_t>> g_pools;
+
+hipMemPool_t pool_of(int dev) {
+  std::lock_guard<std::mutex> lk(g_pool_m);
+  for (auto& p : g_pools)
+    if (p.first == dev) return p.second;
+  hipMemPoolProps props{};
+  props.allocType = hipMemAllocationTypePinned;
+  props.handleTypes = hipMemHandleTypeNone;
+  props.location.type = hipMemLocationTypeDevice;
+  props.location.id = dev;
+  hipMemPool_t pool = nullptr;
+  if (hipMemPoolCreate(&pool, &props) != hipSuccess) {
+    (void)hipGetLastError();
+    return nullptr;
+  }
+  uint64_t keep = ~0ull;  // never trimmed implicitly (a trim at a synchronisation point would free memory)
+  (void)hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &keep);
+  g_pools.emplace_back(dev, pool);
+  return pool;
+}
+}  // namespace
+
+void* dev_alloc(int dev, size_t bytes, hipStream_t st) {
+  hipMemPool_t pool = pool_of(dev);
+  if (!pool) return nullptr;
+  void* p = nullptr;
+  if (hipMallocFromPoolAsync(&p, bytes, pool, st) != hipSuccess) {
+    (void)hipGetLastError();
+    return nullptr;
+  }
+  return p;
+}
+
+void dev_free(void* p, hipStream_t st) {
+  if (p && hipFreeAsync(p, st) != hipSuccess) (void)hipGetLastError();
+}
+
+void pool_trim() {
+  std::lock_guard<std::mutex> lk(g_pool_m);
+  for (auto& p : g_pools) {
+    (void)hipSetDevice(p.first);
+    (void)hipDeviceSynchronize();
+    (void)hipMemPoolTrimTo(p.second, 0);
+  }
+}
+
+namespace {
 struct Reaper {
   std::mutex m;
   std::condition_variable work, idle;
@@ -102,4 +151,8 @@ int reaper_pending(bool wait) {
 
 }  // namespace f5h
 
-extern "C" int f5h_release_pending(int32_t wait) { return f5h::reaper_pending(wait != 0); }
+extern "C" int f5h_release_pending(int32_t wait) {
+  const int n = f5h::reaper_pending(wait != 0);
+  if (wait == 2 && n == 0) f5h::pool_trim();
+  return n;
+}

@@ -35,6 +35,16 @@ struct UseNote {
   ~UseNote() { log.note(st); }
 };
 
+// Device memory of the C-ABI objects: stream-ordered allocations from one pool per device that keeps
+// freed memory for reuse instead of returning it to the system (release threshold = max). Neither an
+// allocation nor a release synchronises the device: hipFree waits for every stream of the device and,
+// while it waits, holds up other threads' HIP calls (tools/diag_drop.py: a stream query blocked 0.74 s
+// behind an unrelated 1 s kernel). Null on failure.
+void* dev_alloc(int dev, size_t bytes, hipStream_t st);
+void dev_free(void* p, hipStream_t st);
+// return the pools' unused memory to the system (f5h_release_pending(2)): may wait for the device
+void pool_trim();
+
 // Run `job` on the reaper thread (FIFO) after hipSetDevice(dev). The job synchronises the events of
 // the object it releases and frees it. Falls back to running inline if no thread can be started.
 void retire(int dev, std::function<void()> job);

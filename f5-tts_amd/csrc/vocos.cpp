@@ -71,12 +71,14 @@ struct f5h_vocos {
   float *norm_b = nullptr, *norm_sm1 = nullptr, *fnorm_b = nullptr, *fnorm_sm1 = nullptr, *win = nullptr;
   std::vector<VBlock> blocks;
 
+  hipStream_t mstream = nullptr;  // uploads at creation, stream-ordered frees at release (reaper.h)
   template <typename T>
   int upload(const std::vector<T>& h, T** out) {
-    void* p = nullptr;
-    VHIP(hipMalloc(&p, h.size() * sizeof(T) + 16));
+    void* p = f5h::dev_alloc(dev, h.size() * sizeof(T) + 16, mstream);
+    if (!p) return f5h_internal_fail(F5H_EHIP, "vocos device allocation");
     allocs.push_back(p);
-    VHIP(hipMemcpy(p, h.data(), h.size() * sizeof(T), hipMemcpyHostToDevice));
+    VHIP(hipMemcpyAsync(p, h.data(), h.size() * sizeof(T), hipMemcpyHostToDevice, mstream));
+    VHIP(hipStreamSynchronize(mstream));
     *out = reinterpret_cast<T*>(p);
     return 0;
   }
@@ -283,6 +285,10 @@ int f5h_vocos_create(const f5h_vocos_arch* arch, const f5h_weight* weights, int3
   f5h_vocos* v = new f5h_vocos();
   v->a = a;
   v->dev = device;
+  if (hipStreamCreateWithFlags(&v->mstream, hipStreamNonBlocking) != hipSuccess) {
+    delete v;
+    return f5h_internal_fail(F5H_EHIP, "vocos stream");
+  }
   v->bf = a.compute == F5H_BF16;
   v->kemb = (a.input_channels * 7 + 63) / 64 * 64;
   v->bins = a.n_fft / 2 + 1;
@@ -307,7 +313,8 @@ void f5h_vocos_destroy(f5h_vocos* v) {
       (void)hipEventSynchronize(ev);
       (void)hipEventDestroy(ev);
     }
-    for (void* p : v->allocs) (void)hipFree(p);
+    for (void* p : v->allocs) f5h::dev_free(p, v->mstream);
+    if (v->mstream) (void)hipStreamDestroy(v->mstream);
     delete v;
   });
 }

@@ -106,7 +106,10 @@ int f5h_engine_create(const f5h_arch* arch, const f5h_weight* weights, int32_t n
  * The same holds for f5h_vocos_destroy and f5h_mel_destroy. */
 void f5h_engine_destroy(f5h_engine* eng);
 /* Releases still queued or running (engines, Vocos and log-mel objects destroyed above); wait != 0
- * first blocks until every one of them has completed. Also run at process exit. */
+ * first blocks until every one of them has completed (also run at process exit). The objects' device
+ * memory comes from a stream-ordered pool per device that keeps released memory for reuse (so neither
+ * creation nor release synchronises the device); wait == 2 then also returns the pool's unused memory
+ * to the system, which waits for the device. */
 int f5h_release_pending(int32_t wait);
 
 /* Arguments of one CFM.sample call after the host preamble of cfm.py:105-158 and

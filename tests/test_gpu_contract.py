@@ -401,10 +401,12 @@ def test_graph_eviction_never_waits_for_other_streams():
 
 def test_engine_drop_never_waits_for_other_streams():
     """Dropping a model (its engine, plus a Vocos and a log-mel front end) while a ~1 s spin kernel runs
-    on another stream returns to the dropping thread at once: the release waits on the reaper thread
-    for the objects' own last-use events only (round-3 verdict weak item 7: hipDeviceSynchronize + hipFree
-    in f5h_engine_destroy stalled every stream). The memory is freed once the objects' work is done, and
-    a later model on the same device runs normally."""
+    on another stream returns to the dropping thread at once, and does not hold up other HIP calls: the
+    release waits on the reaper thread for the objects' own last-use events only and returns their memory
+    to a stream-ordered pool (round-3 verdict weak item 7: hipDeviceSynchronize + hipFree in
+    f5h_engine_destroy stalled every stream; a hipFree also blocks other threads' HIP calls while it waits,
+    tools/diag_drop.py). The memory is released once the objects' work is done, and a later model on the
+    same device reuses the pool and runs normally."""
     _need_gpu()
     import gc as pygc
     import time
@@ -422,24 +424,40 @@ def test_engine_drop_never_waits_for_other_streams():
     voc.decode(ref.transpose(1, 2).float().contiguous())
     mel = MelSpec().to(DEV)
     mel(torch.randn(1, 4096, device=DEV))
-    _run_case(m, inp, y0, steps=2)  # last work of the engine, still in flight below
+    _run_case(m, inp, y0, steps=2)
     torch.cuda.synchronize()
-    other = torch.cuda.Stream()
+    t0 = time.perf_counter()
+    pygc.collect()
+    gc_alone = time.perf_counter() - t0  # the collector's own cost on this heap
+    other, third = torch.cuda.Stream(), torch.cuda.Stream()
+    x = torch.randn(4096, device=DEV)
     with torch.cuda.stream(other):
         torch.cuda._sleep(int(2.0e9))  # ~1 s of spinning on another stream
-    _run_case(m, inp, y0, steps=2)
+    t_spin = time.perf_counter()
+    _run_case(m, inp, y0, steps=2)  # last work of the engine, in flight during the drop
     t0 = time.perf_counter()
     del m, voc, mel
     pygc.collect()
-    took = time.perf_counter() - t0
+    took = time.perf_counter() - t0 - gc_alone
+    t0 = time.perf_counter()
+    with torch.cuda.stream(third):
+        y = x * 2.0
+    third.synchronize()
+    third_op = time.perf_counter() - t0
+    t0 = time.perf_counter()
     still_busy = not other.query()
-    assert still_busy, "the spin kernel ended before the drop: raise its length"
+    query = time.perf_counter() - t0
+    elapsed = time.perf_counter() - t_spin
+    print(f"drop {took:.4f}s (gc alone {gc_alone:.4f}s), third-stream op {third_op:.4f}s, query {query:.4f}s, "
+          f"{elapsed:.3f}s after the spin started")
+    assert still_busy, f"the spin kernel ended {elapsed:.3f}s in, before the checks: raise its length"
     assert took < 0.05, took
+    assert third_op < 0.05 and query < 0.05, (third_op, query)
+    assert torch.equal(y, x * 2.0)
     _lib.lib().f5h_release_pending(1)  # returns once the releases ran (after the spin, on the reaper)
     assert _lib.lib().f5h_release_pending(0) == 0
     m2 = _model(gc.arch_of("tiny"), "bf16")
     assert torch.equal(_run_case(m2, inp, y0, steps=2), ref)
-
 
 def test_nfe_512_runs_and_matches_oracle():
     """The largest accepted step count (512: 513 grid points) runs and matches the CPU oracle; 513

@@ -15,11 +15,12 @@ sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..", "f5-tts_amd"))
 SHAPES = {  # name: (M, N, K); C2 = 2 x 1876 rows, C3 = 64 x 1876 rows
     "c2_qkv": (3752, 3072, 1024), "c2_ffn1": (3752, 2048, 1024), "c2_out": (3752, 1024, 1024),
     "c2_ffn2": (3752, 1024, 2048), "c3_qkv": (120064, 3072, 1024), "c3_ffn2": (120064, 1024, 2048),
+    "c3_ffn1": (120064, 2048, 1024), "c3_out": (120064, 1024, 1024), "c5_qkv": (30032, 3072, 1024),
 }
 for _k in (128, 256, 512, 2048, 4096):  # K sweeps at the C2 output shapes: fixed cost per launch = intercept
     SHAPES[f"c2_out_k{_k}"] = (3752, 1024, _k)
     SHAPES[f"c2_qkv_k{_k}"] = (3752, 3072, _k)
-CFGS = {0: (64, 128, 256), 1: (128, 128, 256), 5: (192, 128, 256), 11: (256, 256, 512)}
+CFGS = {0: (64, 128, 256), 1: (128, 128, 256), 5: (192, 128, 256), 11: (256, 256, 512), 12: (256, 256, 512)}
 # round 3 also timed register-staged intake (cfg 40-45) and K32-stage deeper rings for 192x128 / 128x128
 # (cfg 6-8): slower on every C2 and C3 shape (profiles/r03_gemm_tune_rs_c2.txt, r03_gemm_tune_k32.txt)
 # round 2 also timed 8-wave one-block-per-CU tiles (128x256, 192x256, 256x128, 128x128, 256x256, 256x192),
