@@ -71,10 +71,7 @@ F5H_DEV void attn_block(int& qb, int& bh) {
   bh = id / nqb;
 }
 
-// VAR (A/B, env F5H_ATTN_VAR): bit 0 = the tile row max as four independent max3 chains (depth 6 instead of a
-// 16-deep dependent chain); bit 1 = row sums as two scalar fp32 accumulators, each 16-key chunk summed as a
-// tree (packed fp32 adds beside MFMAs cost ~13 cycles extra each, MI355X_MICROARCH.md 'price of one filler')
-template <typename T, bool PRESCALED, int NW, int VAR = 0>
+template <typename T, bool PRESCALED, int NW>
 __global__ __launch_bounds__(64 * NW, 8 / NW) void attn16_kernel(AttnArgs a) {
   typedef Op16<T> OP;
   typedef typename OP::v8 v8;
@@ -90,6 +87,9 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn16_kernel(AttnArgs a) {
   const int h = lane >> 5;
   int qb, bh;
   attn_block(qb, bh);
+  // with the pad skip, dead query blocks cluster by sequence length: deal the (sequence, head) pairs over
+  // the XCDs round-robin so every XCD holds a share of every length (all blocks of a pair stay on one XCD)
+  if (a.q_len) bh = spread8(bh, gridDim.y);
   const int s_idx = bh / a.H, head = bh - s_idx * a.H;
   const int L = a.L;
   if (a.q_len && qb * (32 * NW) >= a.q_len[s_idx]) {  // dead query block (pad rows only): nothing to write
@@ -147,7 +147,6 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn16_kernel(AttnArgs a) {
   float m_run = 0.f;  // running max (log2 units), valid after tile 0
   f32x16 oacc[2], minit;  // minit: -m_run in every slot, the QK^T chains' first C operand
   f2 lrow = {0.f, 0.f};   // this lane's part of its query's row sum (packed fp32 adds)
-  float lsa = 0.f, lsb = 0.f;  // VAR & 2: the same as two scalar accumulators (chunks 0, 2 and 1, 3)
 #pragma unroll
   for (int r = 0; r < 16; ++r) {
     oacc[0][r] = 0.f;
@@ -245,21 +244,10 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn16_kernel(AttnArgs a) {
           if (kbase + t * 32 + (r & 3) + 8 * (r >> 2) >= klen) sacc[t][r] = -INFINITY;
     }
     float mx = -INFINITY;
-    if constexpr ((VAR & 1) != 0) {
-      float m4[4];
 #pragma unroll
-      for (int c = 0; c < 4; ++c) {
-        m4[c] = -INFINITY;  // (a chain seeded with -inf compiles to v_max3 without operand canonicalisation)
+    for (int t = 0; t < 2; ++t)
 #pragma unroll
-        for (int r = 0; r < 8; ++r) m4[c] = fmaxf(m4[c], sacc[c >> 1][8 * (c & 1) + r]);
-      }
-      mx = fmaxf(fmaxf(m4[0], m4[1]), fmaxf(m4[2], m4[3]));
-    } else {
-#pragma unroll
-      for (int t = 0; t < 2; ++t)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) mx = fmaxf(mx, sacc[t][r]);
-    }
+      for (int r = 0; r < 16; ++r) mx = fmaxf(mx, sacc[t][r]);
     mx = fmaxf(mx, xor32(mx));
     if (kt == 0) {
       // first tile (>= 1 valid key): the running max starts at the tile max
@@ -286,8 +274,6 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn16_kernel(AttnArgs a) {
 #pragma unroll
         for (int r = 0; r < 16; ++r) sacc[t][r] -= d;
       lrow *= alpha;
-      lsa *= alpha;
-      lsb *= alpha;
     }
     // exp2 / pack of 16-key chunk c = (t, sx) of P (row sums from the fp32 exp2s, four packed
     // adds), then its two MFMAs (both O^T halves), issued between chunk c+1's exp2s and packs: a
@@ -296,26 +282,12 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn16_kernel(AttnArgs a) {
     v8 pf[2][2];
     auto exp_chunk = [&](auto C) {
       constexpr int t = decltype(C)::value >> 1, sx = decltype(C)::value & 1;
-      if constexpr ((VAR & 2) != 0) {
-        float e[8];
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          e[j] = __builtin_amdgcn_exp2f(sacc[t][8 * sx + j]);
-          pf[t][sx][j] = from_f32<T>(e[j]);
-        }
-        const float sum = ((e[0] + e[1]) + (e[2] + e[3])) + ((e[4] + e[5]) + (e[6] + e[7]));
-        if constexpr ((decltype(C)::value & 1) == 0)
-          lsa += sum;
-        else
-          lsb += sum;
-      } else {
-#pragma unroll
-        for (int j = 0; j < 8; j += 2) {
-          const f2 e = {__builtin_amdgcn_exp2f(sacc[t][8 * sx + j]), __builtin_amdgcn_exp2f(sacc[t][8 * sx + j + 1])};
-          pf[t][sx][j] = from_f32<T>(e.x);
-          pf[t][sx][j + 1] = from_f32<T>(e.y);
-          lrow += e;
-        }
+      for (int j = 0; j < 8; j += 2) {
+        const f2 e = {__builtin_amdgcn_exp2f(sacc[t][8 * sx + j]), __builtin_amdgcn_exp2f(sacc[t][8 * sx + j + 1])};
+        pf[t][sx][j] = from_f32<T>(e.x);
+        pf[t][sx][j + 1] = from_f32<T>(e.y);
+        lrow += e;
       }
     };
     auto mma_chunk = [&](auto C) {
@@ -354,7 +326,7 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn16_kernel(AttnArgs a) {
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no LDS-DMA outlives the loop (ntile == 0 included)
   probe_mark(a.probe, probe_t, 2);
-  float l_tot = (VAR & 2) ? lsa + lsb : lrow.x + lrow.y;
+  float l_tot = lrow.x + lrow.y;
   l_tot += xor32(l_tot);  // lanes l and l + 32 hold the two key halves of one query
   const float inv = l_tot > 0.f ? 1.f / l_tot : 0.f;
   // Epilogue (T21): lane l < 32 holds columns 8k..8k+3 of its row, lane l + 32 columns 8k+4..8k+7; one
@@ -447,31 +419,14 @@ __global__ __launch_bounds__(64) void attn_f32_kernel(AttnArgs a) {
   probe_exit(a.probe, probe_t);
 }
 
-static int attn_var() {  // F5H_ATTN_VAR: A/B of the row-max / row-sum forms (attn16_kernel VAR)
-  static const int v = [] {
-    const char* e = getenv("F5H_ATTN_VAR");
-    return e ? (atoi(e) & 3) : 0;
-  }();
-  return v;
-}
-
-template <typename T, int VAR>
-static void launch16v(const AttnArgs& a, hipStream_t st) {
+template <typename T>
+static void launch16(const AttnArgs& a, hipStream_t st) {
   constexpr int NW = 8;  // (two 4-wave workgroups per CU measured 40.3 vs 39.6 us at C2: kept one of 8)
   dim3 grid((a.L + 32 * NW - 1) / (32 * NW), a.S * a.H);
   if (a.prescaled)
-    hipLaunchKernelGGL((attn16_kernel<T, true, NW, VAR>), grid, dim3(64 * NW), 0, st, a);
+    hipLaunchKernelGGL((attn16_kernel<T, true, NW>), grid, dim3(64 * NW), 0, st, a);
   else
-    hipLaunchKernelGGL((attn16_kernel<T, false, NW, VAR>), grid, dim3(64 * NW), 0, st, a);
-}
-template <typename T>
-static void launch16(const AttnArgs& a, hipStream_t st) {
-  switch (attn_var()) {
-    case 1: launch16v<T, 1>(a, st); break;
-    case 2: launch16v<T, 2>(a, st); break;
-    case 3: launch16v<T, 3>(a, st); break;
-    default: launch16v<T, 0>(a, st); break;
-  }
+    hipLaunchKernelGGL((attn16_kernel<T, false, NW>), grid, dim3(64 * NW), 0, st, a);
 }
 
 hipError_t attention(int compute, const AttnArgs& a, hipStream_t st) {

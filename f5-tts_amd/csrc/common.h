@@ -243,6 +243,19 @@ template <typename T> F5H_DEV constexpr int elems16() { return 16 / (int)sizeof(
 // be lowered to scratch before the unroller runs).
 // raw buffer descriptor over [p, p + bytes): loads past the extent read 0, stores past it are dropped
 // (the hardware range check), so out-of-range lanes need no branch; bytes < 2^32
+// Bijection on [0, n) that deals the 8 near-equal contiguous chunks of [0, n) (the ranges the XCD-aware
+// block maps give the 8 XCDs) out round-robin: element i of chunk c goes to 8 i + c. Used where the work of
+// an index varies along it (the batch path's pad skip: sequences of different lengths), so that every XCD
+// gets a share of every part instead of one contiguous part.
+F5H_DEV int spread8(int r, int n) {
+  const int q = n >> 3, rem = n & 7;
+  if (q == 0) return r;
+  const int big = rem * (q + 1);
+  const int c = r < big ? r / (q + 1) : rem + (r - big) / q;
+  const int i = r < big ? r - c * (q + 1) : (r - big) - (c - rem) * q;
+  return i * 8 + c;
+}
+
 F5H_DEV __amdgpu_buffer_rsrc_t rsrc_of(const void* p, uint64_t bytes) {
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), 0, (int)(uint32_t)bytes, 0x00020000);
 }

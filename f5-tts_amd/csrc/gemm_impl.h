@@ -527,7 +527,9 @@ __global__ __launch_bounds__(64 * WGM * WGN, 2) void gemm_kernel(GemmArgs g) {
   // XCD, so give each XCD a contiguous run of n-fastest tiles -> its L2 holds whole A panels
   const int nwg = gridDim.x, b = blockIdx.x, xq = nwg >> 3, xr = nwg & 7, xcd = b & 7;
   const int bid = (xcd < xr ? xcd * (xq + 1) : xr * (xq + 1) + (xcd - xr) * xq) + (b >> 3);
-  const int m0 = (bid / ntn) * BM, n0 = (bid % ntn) * BN;
+  // with the pad skip, row tiles of padding cluster by sequence: spread the m-rows over the XCDs
+  const int mrow = g.live_len ? spread8(bid / ntn, (g.M + BM - 1) / BM) : bid / ntn;
+  const int m0 = mrow * BM, n0 = (bid % ntn) * BN;
   if constexpr (EPI == EPI_RESID || EPI == EPI_RESID16) {
     if (!tile_live(g, m0, BM)) {  // every row padding: nothing to add (C2's B = 1 never passes live_len)
       probe_exit(g.probe, probe_t);
@@ -794,7 +796,9 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(GemmArgs g) {
   const int ntn = (g.N + BN - 1) / BN;
   const int nwg = gridDim.x, b = blockIdx.x, xq = nwg >> 3, xr = nwg & 7, xcd = b & 7;
   const int bid = (xcd < xr ? xcd * (xq + 1) : xr * (xq + 1) + (xcd - xr) * xq) + (b >> 3);
-  const int m0 = (bid / ntn) * BM, n0 = (bid % ntn) * BN;
+  // with the pad skip, row tiles of padding cluster by sequence: spread the m-rows over the XCDs
+  const int mrow = g.live_len ? spread8(bid / ntn, (g.M + BM - 1) / BM) : bid / ntn;
+  const int m0 = mrow * BM, n0 = (bid % ntn) * BN;
   if constexpr (EPI == EPI_RESID || EPI == EPI_RESID16) {
     if (!tile_live(g, m0, BM)) {
       probe_exit(g.probe, probe_t);
@@ -994,7 +998,9 @@ __global__ __launch_bounds__(512, 1) void gemm_8p_kernel(GemmArgs g) {
   const int ntn = (g.N + BN - 1) / BN;
   const int nwg = gridDim.x, b = blockIdx.x, xq = nwg >> 3, xr = nwg & 7, xcd = b & 7;
   const int bid = (xcd < xr ? xcd * (xq + 1) : xr * (xq + 1) + (xcd - xr) * xq) + (b >> 3);
-  const int m0 = (bid / ntn) * BM, n0 = (bid % ntn) * BN;
+  // with the pad skip, row tiles of padding cluster by sequence: spread the m-rows over the XCDs
+  const int mrow = g.live_len ? spread8(bid / ntn, (g.M + BM - 1) / BM) : bid / ntn;
+  const int m0 = mrow * BM, n0 = (bid % ntn) * BN;
   if constexpr (EPI == EPI_RESID || EPI == EPI_RESID16) {
     if (!tile_live(g, m0, BM)) {
       probe_exit(g.probe, probe_t);
