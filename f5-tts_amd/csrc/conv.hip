@@ -89,6 +89,23 @@ F5H_DEV void conv_epilogue_any(const ConvArgs& a, const float* Cs, int tid, int 
     conv_epilogue<TC, BP, NT, CP, 1>(a, Cs, tid, s, n0, grp, cg);
 }
 
+// XCD-aware block -> (position block, group, sequence): the hardware deals workgroups round-robin over the 8
+// XCDs, so with the natural grid order every XCD touched every group's 254 KB tap panel (8 L2 misses per
+// panel: conv traffic 3.2x the algorithmic bytes, profiles/r03_pmc_classes.json). The bijective XCD-contiguous
+// remap (cdna_hip_programming.md T1) with the group slowest gives each XCD a contiguous run of whole groups,
+// so a panel leaves MALL/HBM about once.
+F5H_DEV void conv_block(int& pb, int& grp, int& s) {
+  const int npb = gridDim.x, ng = gridDim.y, ns = gridDim.z;
+  const int nwg = npb * ng * ns;
+  const int w = blockIdx.x + npb * (blockIdx.y + ng * blockIdx.z);
+  const int xq = nwg >> 3, xr = nwg & 7, xcd = w & 7;
+  const int id = (xcd < xr ? xcd * (xq + 1) : xr * (xq + 1) + (xcd - xr) * xq) + (w >> 3);
+  grp = id / (ns * npb);
+  const int rem = id - grp * (ns * npb);
+  s = rem / npb;
+  pb = rem - s * npb;
+}
+
 template <int N>
 F5H_DEV void wait_vm() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"i"(N) : "memory");
@@ -110,7 +127,9 @@ __global__ __launch_bounds__(128 * NWM, 1) void conv_kernel(ConvArgs a) {
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid >> 1, wn = wid & 1;
-  const int n0 = blockIdx.x * BP, grp = blockIdx.y, s = blockIdx.z;
+  int pb, grp, s;
+  conv_block(pb, grp, s);
+  const int n0 = pb * BP;
   const int L = a.L, d = a.d;
   const TX* X = reinterpret_cast<const TX*>(a.x);
   const int cg = d / 16;  // channels per group (<= 64; padded to 64 in LDS and in the packed weights)
@@ -244,7 +263,9 @@ __global__ __launch_bounds__(512, 1) void conv16_kernel(ConvArgs a) {
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid >> 1, wn = wid & 1;  // 4 x 64 positions, 2 x 32 channels
-  const int n0 = blockIdx.x * BP, grp = blockIdx.y, s = blockIdx.z;
+  int pb, grp, s;
+  conv_block(pb, grp, s);
+  const int n0 = pb * BP;
   const int L = a.L, d = a.d;
   const TX* X = reinterpret_cast<const TX*>(a.x);
   const int cg = d / 16;  // channels per group (<= 64; padded to 64 in LDS and in the packed weights)
