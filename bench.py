@@ -293,8 +293,11 @@ def class_entry(kc, avg_ms, n, arch, S, L, launches_per_call, ms_call, chains=1,
         if kn:  # operands + result at the operand width (residual read+write for RESID)
             K, Nn = kn
             alg = esz * (S * L * K + Nn * K) + (2 * resid_bytes(arch, esz) if kc in ("out", "ffn2") else esz) * S * L * Nn
-        elif kc == "conv":  # one grouped conv layer: input + output rows + weights (tools/pmc_classes.py)
-            alg = S * L * d * (esz + resid_bytes(arch, esz)) + d * (d // 16) * 31 * esz
+        elif kc == "conv":  # the mean of the two grouped conv layers (tools/pmc_classes.py): layer 1 reads the
+            # fp32 input embedding and writes the operand dtype, layer 2 reads that, the fp32 input embedding
+            # (its residual) and writes the residual stream; plus the 16 groups' 31-tap weights
+            per_elem = ((4 + esz) + (esz + 4 + resid_bytes(arch, esz))) / 2
+            alg = S * L * d * per_elem + d * (d // 16) * 31 * esz
         else:
             alg = 4 * 2 * S * arch["heads"] * L * 64
         e["algorithmic_bytes"] = alg

@@ -61,12 +61,14 @@ def test_pmc_traffic_only_at_the_measured_shape():
 
 
 def test_conv_class_traffic_over_algorithmic():
-    """The conv position embedding class carries its PMC traffic and algorithmic bytes (one grouped conv
-    layer: input + output rows + the 16 groups' 31-tap weights) at the C2 shape."""
+    """The conv position embedding class carries its PMC traffic and algorithmic bytes (the mean of its two
+    grouped conv layers: fp32 input + 16-bit output, then 16-bit input + fp32 residual + 16-bit output; plus
+    the 16 groups' 31-tap weights) at the C2 shape. Since the group-major XCD map (round 4) the measured
+    traffic is ~1.0x that (3.2x before: every XCD re-fetched every group's tap panel)."""
     arch = configs.get_arch("F5TTS_v1_Base")
     e = bench.class_entry("conv", 0.0257, 8, arch, 2, 1876, 16, 50.9, 1)
-    assert e["algorithmic_bytes"] == 2 * 1876 * 1024 * 4 + 1024 * 64 * 31 * 2
-    assert e["traffic"] and 1.0 < e["traffic_over_algorithmic"] < 10.0
+    assert e["algorithmic_bytes"] == 2 * 1876 * 1024 * 7 + 1024 * 64 * 31 * 2
+    assert e["traffic"] and 0.8 < e["traffic_over_algorithmic"] < 1.5
 
 
 # avg launch (us) per class measured by the round-3 final benches (profiles/r03_final_bench_c{2,4,5}.log),

@@ -55,8 +55,9 @@ def algorithmic(c, S=2, L=1876, d=1024, ff=2048, H=16, es=2, rb=2):
         return 4 * es * S * H * L * 64  # q, k, v read + o written
     if c in ("norm", "norm1"):
         return rows * d * (rb + es)
-    if c == "conv":  # one grouped conv layer (31 taps, 16 groups): input + output rows + weights (median of the two)
-        return rows * d * (es + rb) + d * (d // 16) * 31 * es
+    if c == "conv":  # the two grouped conv layers (31 taps, 16 groups), mean: layer 1 fp32 input + operand output,
+        # layer 2 operand input + fp32 residual (the input embedding) + residual-stream output; plus the weights
+        return rows * d * ((4 + es) + (es + 4 + rb)) / 2 + d * (d // 16) * 31 * es
     return None
 
 
