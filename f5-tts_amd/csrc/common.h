@@ -88,6 +88,21 @@ F5H_DEV float gelu_tanh_fast(float x) {  // explicit rounding: identical in ever
   const float u = mul_nc(k0, add_nc(x, mul_nc(k1, x3)));
   return mul_nc(x, __builtin_amdgcn_rcpf(add_nc(1.f, __builtin_amdgcn_exp2f(-u))));
 }
+// The same on a pair of values with packed fp32 VALU (v_pk_mul_f32 / v_pk_add_f32: two elements per
+// instruction, each rounded exactly like the scalar form, so the result is bit for bit gelu_tanh_fast's);
+// the two transcendentals per element stay scalar. Epilogues are VALU-bound on this (FFN1: one exp + one rcp
+// and six arithmetic ops per element with the matrix pipes idle).
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+F5H_DEV f32x2 gelu_tanh_fast2(f32x2 x) {
+#pragma clang fp contract(off)
+  const float k0 = 0.7978845608028654f * 2.f * 1.4426950408889634f, k1 = 0.044715f;
+  const f32x2 x3 = (x * x) * x;
+  const f32x2 u = (x + x3 * k1) * k0;
+  const f32x2 e = {__builtin_amdgcn_exp2f(-u.x), __builtin_amdgcn_exp2f(-u.y)};
+  const f32x2 d = e + 1.f;
+  const f32x2 r = {__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y)};
+  return x * r;
+}
 // ---------------------------------------------------------------- in-kernel launch probe
 // Kernel-side timing of probed launches (f5h_probe_*): the first thread of every workgroup
 // atomicMin's the device wall clock (s_memrealtime, 100 MHz) into start[tick] at entry and

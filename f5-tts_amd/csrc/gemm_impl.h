@@ -428,20 +428,22 @@ F5H_DEV void epilogue_fast_t(const GemmArgs& g, const f32x4 (&acc)[MT][NT], floa
       const RowIn& ri = rbuf[i & 1][t];
       if constexpr (EPI == EPI_QKV) {
         const V8 cs = as_v8(ri);
+        // interleaved pairs (a, b) -> (a c - b s, b c + a s) as packed products and one packed add (each
+        // element rounded as rope_re / rope_im round it), then the q scale on pairs
 #pragma unroll
-        for (int pr = 0; pr < 2; ++pr) {
-          const float c0 = cs.v[4 * pr + 0], s0 = cs.v[4 * pr + 1];
-          const float c1 = cs.v[4 * pr + 2], s1 = cs.v[4 * pr + 3];
-          const float a0_ = x.v[4 * pr + 0], a1_ = x.v[4 * pr + 1], b0 = x.v[4 * pr + 2], b1 = x.v[4 * pr + 3];
-          const float r0 = rope_re(a0_, a1_, c0, s0), r1 = rope_im(a0_, a1_, c0, s0);
-          const float r2 = rope_re(b0, b1, c1, s1), r3 = rope_im(b0, b1, c1, s1);
-          x.v[4 * pr + 0] = rope_on ? r0 : a0_;
-          x.v[4 * pr + 1] = rope_on ? r1 : a1_;
-          x.v[4 * pr + 2] = rope_on ? r2 : b0;
-          x.v[4 * pr + 3] = rope_on ? r3 : b1;
+        for (int p = 0; p < 4; ++p) {
+          const float c = cs.v[2 * p], sn = cs.v[2 * p + 1];
+          const f32x2 ab = {x.v[2 * p], x.v[2 * p + 1]};
+          f32x2 r;
+          {
+#pragma clang fp contract(off)
+            const f32x2 pc = ab * c, ps = f32x2{ab.y, ab.x} * sn;
+            r = pc + f32x2{-ps.x, ps.y};
+            r = (rope_on ? r : ab) * qsc;  // exact for qsc = 1 (k, v columns)
+          }
+          x.v[2 * p] = r.x;
+          x.v[2 * p + 1] = r.y;
         }
-#pragma unroll
-        for (int e = 0; e < 8; ++e) x.v[e] = mul_nc(x.v[e], qsc);  // exact for qsc = 1 (k, v columns)
         const int sq = fdiv(row, g.seq_len), pos = row - sq * g.seq_len;
         store8_rs<TC>(dst, (uint32_t)((((int64_t)sq * g.heads + head) * g.seq_len + pos) * 64 + dh), x);
       } else if constexpr (EPI == EPI_RESID || EPI == EPI_RESID16) {
@@ -456,10 +458,17 @@ F5H_DEV void epilogue_fast_t(const GemmArgs& g, const f32x4 (&acc)[MT][NT], floa
         for (int e = 0; e < 8; ++e) o.v[e] = resid_add(c.v[e], gate8.v[e], x.v[e], keep);
         store8_rs<ResT<TC, EPI>>(dst, (uint32_t)((int64_t)row * g.ldc + col), o);
       } else if constexpr (EPI == EPI_GELU_TANH || EPI == EPI_GELU_ERF_OP) {
+        if constexpr (EPI == EPI_GELU_TANH && is16<TC>()) {
 #pragma unroll
-        for (int e = 0; e < 8; ++e)
-          x.v[e] = EPI == EPI_GELU_ERF_OP ? gelu_erf(x.v[e])
-                                          : (is16<TC>() ? gelu_tanh_fast(x.v[e]) : gelu_tanh(x.v[e]));
+          for (int e = 0; e < 8; e += 2) {
+            const f32x2 gv = gelu_tanh_fast2(f32x2{x.v[e], x.v[e + 1]});
+            x.v[e] = gv.x;
+            x.v[e + 1] = gv.y;
+          }
+        } else {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) x.v[e] = EPI == EPI_GELU_ERF_OP ? gelu_erf(x.v[e]) : gelu_tanh(x.v[e]);
+        }
         store8_rs<TC>(dst, (uint32_t)((int64_t)row * g.ldc + col), x);
       } else if constexpr (EPI == EPI_STORE16) {
         store8_rs<TC>(dst, (uint32_t)((int64_t)row * g.ldc + col), x);

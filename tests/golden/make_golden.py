@@ -265,6 +265,17 @@ def main():
     # (16-bit residual stream) and the masked batch path
     jobs["e2_base_sample_b2_fp16"] = sample_job(e2, gc.E2B2, 2, dtype=torch.float16)
     jobs["base_batch_sample_b4_masked_fp16"] = sample_job(base_masked, gc.BASE_B4, 2, dtype=torch.float16)
+    def c3_pair_job():
+        # the C3 pair (golden_cases.C3_PAIR): sliced out of the B=32 C3 inputs, reference B=2 batch at 1876 frames
+        model = build_ref(base)
+        _, pair = gc.c3_pair_inputs()
+        with fp32_noise(), torch.no_grad():
+            out, traj = model.sample(cond=pair["cond"], text=pair["text"], duration=pair["duration"],
+                                     lens=pair["lens"], steps=gc.C3_PAIR_NFE, cfg_strength=2.0,
+                                     sway_sampling_coef=-1.0, seed=7)
+        return dict(out=out.float().numpy(), traj_1=traj[1].float().numpy(), checksum=checksum(pair))
+
+    jobs["c3_pair_sample_fp32"] = c3_pair_job
     if not args.skip_c2:
         c2 = configs.get_arch("F5TTS_v1_Base")
         jobs["c2_sample_fp32"] = sample_job(c2, gc.C2, 16)

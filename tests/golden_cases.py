@@ -24,6 +24,25 @@ E2B2 = dict(B=2, ref_frames=[100, 60], total_frames=[300, 220], n_text=[50, 40])
 BASE_B4 = dict(B=4, ref_frames=[120, 200, 80, 150], total_frames=[400, 520, 260, 450], n_text=[60, 90, 40, 70])
 
 
+# C3 at full length (round 4): the shortest and the longest utterance of the C3 batch (synthetic.c3_case,
+# make_case seed 1234), sliced out of the B=32 inputs, run by the reference as a B=2 batch padded to 1876
+# frames (the batch-mask path). The GPU tests pin the engine on this pair against the reference and then the
+# full B=32 C3 batch to the pair bit for bit (sequences of one padded length are independent).
+C3_PAIR = (0, 31)
+C3_PAIR_NFE = 2
+
+
+def c3_pair_inputs():
+    """The C3 batch inputs (B=32) and the pair slice: (full, pair) dicts of cond/text/lens/duration."""
+    from f5_tts_amd import synthetic
+
+    c3 = synthetic.c3_case()
+    full = synthetic.make_case(B=c3["B"], ref_frames=c3["ref"], total_frames=c3["total"], n_text=c3["nt"])
+    idx = list(C3_PAIR)
+    pair = {k: v[idx] for k, v in full.items()}
+    return full, pair
+
+
 def arch_of(tag):
     if tag == "tiny":
         return configs.get_arch("DiT_tiny", text_num_embeds=64)

@@ -455,3 +455,36 @@ def test_pad_row_skip_bitwise_at_c3_shape(masked):
     b, tb = _sample_pad_skip(m, "bf16", inp, y0, dur, 3, True, keep_trajectory=True)
     assert torch.isfinite(b).all()
     assert torch.equal(a, b) and torch.equal(ta, tb)
+
+
+@pytest.mark.parametrize("compute", ["fp32", "bf16"])
+def test_c3_full_batch_pinned_through_the_reference_pair(compute):
+    """C3 at full size (Base, B=32, 564..1876 frames padded to 1876, batch-mask path), pinned to the reference:
+    the shortest and the longest utterance of the batch, run by the reference as a B=2 batch at 1876 frames
+    (tests/golden/c3_pair_sample_fp32.npz), match the fp32 engine <= 1e-3 (max-rel); and in both modes the
+    full B=32 batch's rows of those utterances equal the engine's B=2 run bit for bit (sequences of one padded
+    length never interact, in the reference as here: cfm.py:155-158, modules.py:511-553)."""
+    _need_gpu()
+    from f5_tts_amd import configs
+
+    m = _model(configs.get_arch("F5TTS_v1_Base"), compute)
+    full, pair = gc.c3_pair_inputs()
+    kw = dict(steps=gc.C3_PAIR_NFE, cfg_strength=2.0, sway_sampling_coef=-1.0, keep_trajectory=False)
+
+    def run(inp):
+        y0 = synthetic.reference_noise(inp["duration"], gc.SEED)
+        out, _ = m.sample(cond=inp["cond"].to(DEV), text=inp["text"].to(DEV), duration=inp["duration"],
+                          lens=inp["lens"], y0=y0.to(DEV), **kw)
+        torch.cuda.synchronize()
+        return out
+
+    out_pair = run(pair)
+    out_full = run(full)
+    assert torch.isfinite(out_full).all()
+    assert torch.equal(out_full[list(gc.C3_PAIR)], out_pair)
+    if compute == "fp32":
+        ref = gc.load("c3_pair_sample_fp32")
+        assert ref is not None
+        got = out_pair.float().cpu().numpy()
+        err = np.abs(got - ref["out"]).max() / np.abs(ref["out"]).max()
+        assert err <= FP32_TOL, err

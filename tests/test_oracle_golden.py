@@ -100,3 +100,19 @@ def test_reference_bf16_envelope_recorded():
     e_b = gc.rel_err(b16["out"][:, gen], f32["out"][:, gen])
     e_h = gc.rel_err(f16["out"][:, gen], f32["out"][:, gen])
     assert 5e-3 < e_b < 0.2 and e_h < e_b
+
+
+def test_oracle_c3_pair_matches_reference(torch_threads):
+    """The C3 pair fixture (the shortest and the longest utterance of the C3 batch as a B=2 batch at 1876
+    frames, Base, NFE 2; golden_cases.C3_PAIR): the oracle reproduces the reference's own output."""
+    g = gc.load("c3_pair_sample_fp32")
+    assert g is not None
+    arch = gc.arch_of("c2")
+    W = synthetic.make_weights_torch(arch)
+    _, pair = gc.c3_pair_inputs()
+    np.testing.assert_allclose([float(pair["cond"].double().sum()), float(pair["text"].sum())], g["checksum"],
+                               rtol=1e-12)
+    out, traj = ref_cpu.cfm_sample(W, arch, pair["cond"], pair["text"], pair["duration"], lens=pair["lens"],
+                                   steps=gc.C3_PAIR_NFE, cfg_strength=2.0, sway_sampling_coef=-1.0, seed=gc.SEED)
+    assert gc.max_rel(traj[1].numpy(), g["traj_1"]) < SAMPLE_TOL
+    assert gc.max_rel(out.numpy(), g["out"]) < SAMPLE_TOL
