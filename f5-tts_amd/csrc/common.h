@@ -80,13 +80,21 @@ F5H_DEV float sub_nc(float a, float b) {
   return a - b;
 }
 
+// x as the fp32 op that produced it rounded it: an opaque move, so hipcc cannot fold that op (a multiply)
+// into a later 16-bit conversion (v_fma_mix rounds the product once, straight to fp16, where the fast
+// epilogues' packed forms round it to fp32 first; tile configs must agree bit for bit)
+F5H_DEV float rounded(float x) {
+  asm volatile("" : "+v"(x));
+  return x;
+}
+
 // bf16-mode form: 0.5x(1+tanh(u)) == x * sigmoid(2u) = x / (1 + 2^(-2u*log2 e)); v_exp_f32 + v_rcp_f32
 // (rel. error ~1e-6, far below the bf16 rounding of the result; the fp32 parity mode keeps tanhf)
 F5H_DEV float gelu_tanh_fast(float x) {  // explicit rounding: identical in every kernel that inlines it
   const float k0 = 0.7978845608028654f * 2.f * 1.4426950408889634f, k1 = 0.044715f;
   const float x3 = mul_nc(mul_nc(x, x), x);
   const float u = mul_nc(k0, add_nc(x, mul_nc(k1, x3)));
-  return mul_nc(x, __builtin_amdgcn_rcpf(add_nc(1.f, __builtin_amdgcn_exp2f(-u))));
+  return rounded(mul_nc(x, __builtin_amdgcn_rcpf(add_nc(1.f, __builtin_amdgcn_exp2f(-u)))));
 }
 // The same on a pair of values with packed fp32 VALU (v_pk_mul_f32 / v_pk_add_f32: two elements per
 // instruction, each rounded exactly like the scalar form, so the result is bit for bit gelu_tanh_fast's);
@@ -146,7 +154,7 @@ F5H_DEV void probe_exit(const f5h::DevProbe& p, const ProbeT& r) {
 }
 
 F5H_DEV float gelu_erf(float x) {  // nn.GELU(), modules.py:266 (explicit rounding, see gelu_tanh_fast)
-  return mul_nc(mul_nc(0.5f, x), add_nc(1.f, erff(mul_nc(x, 0.7071067811865476f))));
+  return rounded(mul_nc(mul_nc(0.5f, x), add_nc(1.f, erff(mul_nc(x, 0.7071067811865476f)))));
 }
 F5H_DEV float softplus(float x) {  // torch softplus (threshold 20)
   return x > 20.f ? x : log1pf(expf(x));

@@ -81,3 +81,19 @@ def test_attention_asm_builds_without_scratch(tmp_path):
         if m:
             sizes[m.group(1)] = int(m.group(2))
     assert len(sizes) >= 2 and all(v == 0 for v in sizes.values()), sizes
+
+
+def test_fp16_gemm_epilogues_round_through_fp32(tmp_path):
+    """No fp16 GEMM instance folds an epilogue product into its fp16 conversion (v_fma_mix rounds the
+    product once, straight to fp16; the packed fast epilogues round it to fp32 first), so every tile
+    configuration stores the same bits (test_sample_bitwise_identical_across_tile_configs[fp16])."""
+    lines = _asm("gemm_f16_a.hip", tmp_path)
+    cur, kernels, mixed = None, 0, set()
+    for ln in lines:
+        m = re.match(r"^(_Z\S*gemm\S*_kernel\S*):(\s|$)", ln)
+        if m:
+            cur = m.group(1)
+            kernels += 1
+        elif cur and "v_fma_mix" in ln:
+            mixed.add(cur)
+    assert kernels >= 10 and not mixed, (kernels, sorted(mixed))

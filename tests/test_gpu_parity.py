@@ -99,14 +99,17 @@ def test_op_linear_every_tile_config(M, N, K, compute):
         assert torch.equal(C, outs[0]), cfg
 
 
-def test_sample_bitwise_identical_across_tile_configs():
+@pytest.mark.parametrize("compute", ["bf16", "fp16"])
+def test_sample_bitwise_identical_across_tile_configs(compute):
     """All GEMM epilogues (QKV+RoPE, gated residual, GELU, input projection) under every tile
-    configuration: a Base-architecture sample is bitwise identical."""
+    configuration: a Base-architecture sample is bitwise identical. fp16 also pins the epilogue
+    rounding: no config may fold a product into its fp16 conversion (v_fma_mix) where another rounds
+    it to fp32 first."""
     _need_gpu()
     from f5_tts_amd import configs
 
     arch = configs.get_arch("F5TTS_v1_Base")
-    m = _model(arch, "bf16")
+    m = _model(arch, compute)
     inp = synthetic.make_case(B=2, ref_frames=[200, 150], total_frames=[700, 610], n_text=[90, 70])
     dur = torch.tensor([700, 610])
     y0 = synthetic.reference_noise(dur, 5)
