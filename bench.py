@@ -60,17 +60,20 @@ def seq_flops(arch, N):
     return per_tok * L + 4.0 * depth * d * L * L
 
 
-def _same_shape(a, b):
-    """Launch shapes agree on S, L, dim, depth (and on the workload when both name one)."""
+def _same_shape(a, b, match_compute=True):
+    """Launch shapes agree on S, L, dim, depth (and on the workload when both name one); timings also on
+    the compute dtype (summaries without one were measured in bf16: fp16 runs at a lower clock)."""
     if not a or not b:
         return False
     keys = ("S", "L", "dim", "depth")
     if any(a.get(k) != b.get(k) for k in keys):
         return False
+    if match_compute and a.get("compute", "bf16") != b.get("compute", "bf16"):
+        return False
     return a.get("config") is None or b.get("config") is None or a["config"] == b["config"]
 
 
-def profile_class(pattern, kernel_class, shape):
+def profile_class(pattern, kernel_class, shape, match_compute=True):
     """A kernel class's entry in the newest committed profile summary (profiles/<pattern>, written by
     tools/pmc_classes.py or tools/class_profile.py) measured at this launch shape, and its source file.
     Summaries of other shapes are never attached (None, reason)."""
@@ -80,7 +83,7 @@ def profile_class(pattern, kernel_class, shape):
         return None, None
     for f in reversed(files):
         d = json.load(open(f))
-        if _same_shape(d.get("shape"), shape):
+        if _same_shape(d.get("shape"), shape, match_compute):
             return d.get("classes", {}).get(kernel_class), os.path.relpath(f, REPO)
     return None, f"no profiles/{pattern} summary at shape {shape} (newest: {os.path.relpath(files[-1], REPO)})"
 
@@ -89,8 +92,8 @@ def pmc_traffic(kernel_class, shape):
     """HBM bytes per launch of a kernel class from the newest committed rocprofv3 PMC summary at this
     launch shape (profiles/*_pmc_classes.json, tools/pmc_classes.py: separate FETCH_SIZE and WRITE_SIZE
     passes, 2 x FETCH_SIZE (gfx950 counts half of wide streaming reads, MI355X_MICROARCH.md §HBM) +
-    WRITE_SIZE), and its source file; other shapes get None."""
-    ent, src = profile_class("*_pmc_classes*.json", kernel_class, shape)
+    WRITE_SIZE), and its source file; other shapes get None. Bytes do not depend on the 16-bit type."""
+    ent, src = profile_class("*_pmc_classes*.json", kernel_class, shape, match_compute=False)
     return (ent["hbm_bytes"] if ent else None), src
 
 
@@ -249,7 +252,7 @@ PROBE_CLASSES = ("qkv", "attention", "out", "norm", "ffn1", "ffn2", "conv")
 PEAK_HBM_GBPS = 8000.0
 
 
-def class_entry(kc, avg_ms, n, arch, S, L, launches_per_call, ms_call, chains=1, config=None, esz=2):
+def class_entry(kc, avg_ms, n, arch, S, L, launches_per_call, ms_call, chains=1, config=None, esz=2, compute="bf16"):
     """One kernel class: algorithmic work per launch slot / average launch span. With the two CFG
     chains captured in parallel (chains = 2, F5H_SPLIT_CFG=1) each chain launches the class
     on half the sequences and the two chains' launches of a class overlap in time, so a slot (the span
@@ -268,7 +271,7 @@ def class_entry(kc, avg_ms, n, arch, S, L, launches_per_call, ms_call, chains=1,
         ach = by / (avg_ms * 1e-3) / 1e9 if by else 0.0
         e.update(bound="hbm", achieved=round(ach, 1), peak=PEAK_HBM_GBPS, unit="GB/s",
                  frac=round(ach / PEAK_HBM_GBPS, 4), bytes_per_launch=by)
-    shape = {"S": S, "L": L, "dim": arch["dim"], "depth": arch["depth"], "config": config}
+    shape = {"S": S, "L": L, "dim": arch["dim"], "depth": arch["depth"], "config": config, "compute": compute}
     traffic, src = pmc_traffic(kc, shape)
     e["traffic"] = traffic
     e["traffic_source"] = src
@@ -550,7 +553,7 @@ def run_rank(args):
         eng.probe(None)
         if n:
             classes[kc] = class_entry(kc, ms / n, n, arch, S, L, launches[kc] * case["nfe"], ms_pre, chains,
-                                      config=args.config, esz=esz)
+                                      config=args.config, esz=esz, compute=args.compute)
     probe = args.probe
     if probe == "auto":
         probe = max(classes, key=lambda k: classes[k]["share_of_call"] or 0.0) if classes else "none"
@@ -566,7 +569,8 @@ def run_rank(args):
         eng.probe(None)
         if n_launch:
             roof = class_entry(probe, probe_ms / n_launch, n_launch, arch, S, L, launches[probe] * case["nfe"],
-                               elapsed / args.steps * 1e3, chains, config=args.config, esz=esz)
+                               elapsed / args.steps * 1e3, chains, config=args.config, esz=esz,
+                               compute=args.compute)
             roof["timing"] = ("in-kernel s_memrealtime stamps: first workgroup start to last wave end of every "
                               "launch of the class in every 4th ODE step inside the timed region (rank 0); "
                               "rocprof_* = the committed rocprofv3 kernel-trace average of the class at this shape")

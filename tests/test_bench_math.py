@@ -60,6 +60,18 @@ def test_pmc_traffic_only_at_the_measured_shape():
     assert t is None and "no profiles" in src
 
 
+def test_timing_summaries_only_for_the_measured_compute_type():
+    """The committed kernel-trace averages and SQ counters (measured in bf16) are attached to a bf16 line
+    only: an fp16 line at the same shape gets neither (fp16 runs the same cycles at a lower clock), while
+    the byte traffic, which does not depend on the 16-bit type, is attached to both."""
+    arch = configs.get_arch("F5TTS_v1_Base")
+    bf = bench.class_entry("attention", 0.036, 8, arch, 2, 1876, 352, 52.0, 1, config="c2", compute="bf16")
+    fp = bench.class_entry("attention", 0.037, 8, arch, 2, 1876, 352, 52.0, 1, config="c2", compute="fp16")
+    assert "rocprof_frac" in bf and "pmc" in bf
+    assert "rocprof_frac" not in fp and "pmc" not in fp
+    assert bf["traffic"] and fp["traffic"] == bf["traffic"]
+
+
 def test_conv_class_traffic_over_algorithmic():
     """The conv position embedding class carries its PMC traffic and algorithmic bytes (the mean of its two
     grouped conv layers: fp32 input + 16-bit output, then 16-bit input + fp32 residual + 16-bit output; plus
