@@ -252,13 +252,34 @@ PROBE_CLASSES = ("qkv", "attention", "out", "norm", "ffn1", "ffn2", "conv")
 PEAK_HBM_GBPS = 8000.0
 
 
-def class_entry(kc, avg_ms, n, arch, S, L, launches_per_call, ms_call, chains=1, config=None, esz=2, compute="bf16"):
+def live_flops(kc, arch, L, qlens):
+    """Algorithmic FLOPs of one launch when the pad-row skip is on (batch path, B > 1): pad query rows' attention
+    output is zeroed after to_out (modules.py:551-553), so attention needs only the live query rows (against all
+    L keys, or the sequence's own keys with attn_mask_enabled) and the out-projection only the live rows; the other
+    classes need every row (pad rows' K/V and hidden states feed live rows of the next layer). None: no change."""
+    d = arch["dim"]
+    if kc == "attention":
+        keys = qlens if arch.get("attn_mask_enabled") else [L] * len(qlens)
+        return 4.0 * arch["heads"] * 64 * sum(q * k for q, k in zip(qlens, keys))
+    if kc == "out":
+        return 2.0 * sum(qlens) * d * d
+    return None
+
+
+def class_entry(kc, avg_ms, n, arch, S, L, launches_per_call, ms_call, chains=1, config=None, esz=2, compute="bf16",
+                qlens=None):
     """One kernel class: algorithmic work per launch slot / average launch span. With the two CFG
     chains captured in parallel (chains = 2, F5H_SPLIT_CFG=1) each chain launches the class
     on half the sequences and the two chains' launches of a class overlap in time, so a slot (the span
     of one launch) covers both halves: flops are counted for all S sequences and the slot count is per
-    chain."""
+    chain. qlens (per-sequence lengths, CFG copies included) when the pad-row skip runs: attention and the
+    out-projection are priced on their live rows (the padded count stays in padded_flops_per_launch)."""
     fl = class_flops(kc, arch, S, L)
+    padded = None
+    if fl and qlens is not None and len(set(qlens)) > 1:
+        lf = live_flops(kc, arch, L, qlens)
+        if lf is not None:
+            padded, fl = fl, lf
     e = {"kernel": kc, "avg_launch_us": round(avg_ms * 1e3, 3), "sampled_launches": n,
          "launches_per_call": launches_per_call, "cfg_chains": chains,
          "share_of_call": round(avg_ms * launches_per_call / ms_call, 4) if ms_call else None}
@@ -266,6 +287,9 @@ def class_entry(kc, avg_ms, n, arch, S, L, launches_per_call, ms_call, chains=1,
         ach = fl / (avg_ms * 1e-3) / 1e12
         e.update(bound="mfma", achieved=round(ach, 2), peak=PEAK_BF16_TFLOPS, unit="TFLOP/s",
                  frac=round(ach / PEAK_BF16_TFLOPS, 4), flops_per_launch=fl)
+        if padded is not None:
+            e["padded_flops_per_launch"] = padded
+            e["flops_basis"] = "live rows (pad-row skip): attention queries / out-proj rows of each sequence's length"
     else:
         by = class_bytes(kc, arch, S, L, esz)
         ach = by / (avg_ms * 1e-3) / 1e9 if by else 0.0
@@ -532,6 +556,10 @@ def run_rank(args):
     for kc in ("qkv", "attention", "out", "ffn1", "ffn2"):
         launches[kc] = arch["depth"]
     launches["conv"] = 1
+    # the pad-row skip runs on the batch path (B > 1, one bucket): attention and out-proj work on live rows
+    qlens = None
+    if B > 1 and len(batches) == 1 and os.environ.get("F5H_NO_PAD_SKIP") != "1":
+        qlens = [utts[i]["total"] for i in batches[0]] * (S // B)
 
     for _ in range(args.warmup):
         step()
@@ -553,7 +581,7 @@ def run_rank(args):
         eng.probe(None)
         if n:
             classes[kc] = class_entry(kc, ms / n, n, arch, S, L, launches[kc] * case["nfe"], ms_pre, chains,
-                                      config=args.config, esz=esz, compute=args.compute)
+                                      config=args.config, esz=esz, compute=args.compute, qlens=qlens)
     probe = args.probe
     if probe == "auto":
         probe = max(classes, key=lambda k: classes[k]["share_of_call"] or 0.0) if classes else "none"
@@ -570,7 +598,7 @@ def run_rank(args):
         if n_launch:
             roof = class_entry(probe, probe_ms / n_launch, n_launch, arch, S, L, launches[probe] * case["nfe"],
                                elapsed / args.steps * 1e3, chains, config=args.config, esz=esz,
-                               compute=args.compute)
+                               compute=args.compute, qlens=qlens)
             roof["timing"] = ("in-kernel s_memrealtime stamps: first workgroup start to last wave end of every "
                               "launch of the class in every 4th ODE step inside the timed region (rank 0); "
                               "rocprof_* = the committed rocprofv3 kernel-trace average of the class at this shape")

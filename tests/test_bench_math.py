@@ -156,3 +156,20 @@ def test_cpu_baseline_extrapolates_batch_configs():
     assert c["seconds"] > c["per_step_s"] * 8  # (fixed + NFE x step) x B/b
     c = bench.cpu_baseline("c1", dict(case, B=1, ref=20, total=48, nt=8), arch, threads=2)
     assert c["extrapolated"] is False and c["value"] > 0
+
+
+def test_pad_skip_prices_attention_and_out_on_live_rows():
+    """With the pad-row skip (C3: mixed lengths) the attention class is priced on live query rows against all
+    keys and the out-projection on live rows; QKV/FFN keep every row; equal lengths change nothing."""
+    arch = configs.get_arch("F5TTS_v1_Base")
+    q = [1876, 564, 1200, 900] * 2  # B = 4, CFG copies
+    S, L = len(q), 1876
+    a = bench.class_entry("attention", 1.0, 8, arch, S, L, 22, 100.0, qlens=q)
+    assert a["flops_per_launch"] == 4.0 * 16 * 64 * L * sum(q)
+    assert a["padded_flops_per_launch"] == bench.class_flops("attention", arch, S, L) > a["flops_per_launch"]
+    o = bench.class_entry("out", 1.0, 8, arch, S, L, 22, 100.0, qlens=q)
+    assert o["flops_per_launch"] == 2.0 * sum(q) * 1024 * 1024
+    f = bench.class_entry("ffn1", 1.0, 8, arch, S, L, 22, 100.0, qlens=q)
+    assert f["flops_per_launch"] == bench.class_flops("ffn1", arch, S, L) and "padded_flops_per_launch" not in f
+    same = bench.class_entry("attention", 1.0, 8, arch, S, L, 22, 100.0, qlens=[L] * S)
+    assert same["flops_per_launch"] == bench.class_flops("attention", arch, S, L)
