@@ -106,22 +106,26 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn16_kernel(AttnArgs a) {
 
   const int qrow = qb * (32 * NW) + wid * 32 + (lane & 31);
 
-  // ---- LDS-DMA of a K/V tile: chunk p = (r*NW + w)*64 + lane of the 64-row x 8-chunk image
-  int dsrc[CPW];
+  // ---- LDS-DMA of a K/V tile: chunk p = (r*NW + w)*64 + lane of the 64-row x 8-chunk image, by
+  // buffer_load ... lds: the lane's byte offset in the tile is fixed (voffset), the tile's is a scalar
+  // (soffset), the LDS destination a scalar (M0), so a tile's DMA costs no vector instructions; rows past L
+  // are outside the buffer and read as zero (their keys are masked, their P is 0)
+  const int wid_s = __builtin_amdgcn_readfirstlane(wid);
+  const __amdgpu_buffer_rsrc_t krs = rsrc_of(K, L * 128);
+  const __amdgpu_buffer_rsrc_t vrs = rsrc_of(V, L * 128);
+  uint32_t dvoff[CPW];
 #pragma unroll
   for (int r = 0; r < CPW; ++r) {
     const int p = (r * NW + wid) * 64 + lane, row = p >> 3, slot = p & 7;
-    dsrc[r] = swz128(row, slot) * 8;  // element offset of the source chunk inside its row
+    dvoff[r] = (uint32_t)(row * 128 + swz128(row, slot) * 16);  // bytes: row, swizzled source chunk
   }
   auto dma = [&](int buf, int kt) {
     uint4* Ks = lds + buf * (TILE_B / 16);
     uint4* Vs = Ks + 512;
 #pragma unroll
     for (int r = 0; r < CPW; ++r) {
-      const int row = ((r * NW + wid) * 64 + lane) >> 3;
-      const int64_t off = (int64_t)min(kt * 64 + row, L - 1) * 64 + dsrc[r];
-      __builtin_amdgcn_global_load_lds((const void*)(K + off), (LDS_PTR(void))(Ks + (r * NW + wid) * 64), 16, 0, 0);
-      __builtin_amdgcn_global_load_lds((const void*)(V + off), (LDS_PTR(void))(Vs + (r * NW + wid) * 64), 16, 0, 0);
+      dma16(krs, (LDS_PTR(void))(Ks + (r * NW + wid_s) * 64), dvoff[r], kt * 8192);
+      dma16(vrs, (LDS_PTR(void))(Vs + (r * NW + wid_s) * 64), dvoff[r], kt * 8192);
     }
   };
 
@@ -183,7 +187,8 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn16_kernel(AttnArgs a) {
       for (int j = 0; j < 8; ++j) qf[ks][j] = from_f32<T>(to_f32(qf[ks][j]) * c);
     }
   }
-  for (int kt = 0; kt < ntile; ++kt) {
+  // the tile loop unrolled by the ring depth, so a tile's slot (and every LDS read offset) is a constant
+  auto tile = [&](auto SLOT, const int kt) {
     // tile kt landed for this wave's own DMA (tile kt+1 may stay in flight); the barrier
     // publishes every wave's part of it and retires all reads of slot (kt+3)%4 (= tile kt-1).
     if (kt + 2 < ntile)
@@ -194,15 +199,16 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn16_kernel(AttnArgs a) {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     if (kt == 0) probe_mark(a.probe, probe_t, 1);
-    const uint32_t so = (uint32_t)((kt % NS) * TILE_B);
+    constexpr int slot = decltype(SLOT)::value;
+    constexpr uint32_t so = (uint32_t)(slot * TILE_B);  // ring slot offset: an immediate of every LDS read
 
     u32x4 kf[2][4];
     static_for<0, 4>([&](auto KS) {
       constexpr int ks = decltype(KS)::value;
-      kf[0][ks] = lds_b128<0>(kaddr[ks] + so);
-      kf[1][ks] = lds_b128<4096>(kaddr[ks] + so);
+      kf[0][ks] = lds_b128<so>(kaddr[ks]);
+      kf[1][ks] = lds_b128<so + 4096>(kaddr[ks]);
     });
-    if (kt + 3 < ntile) dma((kt + 3) % NS, kt + 3);
+    if (kt + 3 < ntile) dma((slot + 3) % NS, kt + 3);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 #pragma unroll
     for (int t = 0; t < 2; ++t)
@@ -216,8 +222,8 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn16_kernel(AttnArgs a) {
         constexpr int t = decltype(TT)::value;
         static_for<0, 2>([&](auto S) {
           constexpr int sx = decltype(S)::value;
-          vf[u][t][sx][0] = lds_tr_b64<(32 * t + 16 * sx) * 128>(vaddr[u][0] + so);
-          vf[u][t][sx][1] = lds_tr_b64<(32 * t + 16 * sx) * 128>(vaddr[u][1] + so);
+          vf[u][t][sx][0] = lds_tr_b64<so + (32 * t + 16 * sx) * 128>(vaddr[u][0]);
+          vf[u][t][sx][1] = lds_tr_b64<so + (32 * t + 16 * sx) * 128>(vaddr[u][1]);
         });
       });
     };
@@ -323,6 +329,12 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn16_kernel(AttnArgs a) {
       __builtin_amdgcn_sched_barrier(0);
     });
     mma_chunk(std::integral_constant<int, 3>{});
+  };
+  for (int kt0 = 0; kt0 < ntile; kt0 += NS) {
+    static_for<0, NS>([&](auto S) {
+      const int kt = kt0 + decltype(S)::value;
+      if (kt < ntile) tile(S, kt);
+    });
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no LDS-DMA outlives the loop (ntile == 0 included)
   probe_mark(a.probe, probe_t, 2);

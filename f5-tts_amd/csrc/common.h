@@ -282,6 +282,12 @@ F5H_DEV int spread8(int r, int n) {
 F5H_DEV __amdgpu_buffer_rsrc_t rsrc_of(const void* p, uint64_t bytes) {
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), 0, (int)(uint32_t)bytes, 0x00020000);
 }
+// one 16-byte-per-lane LDS-DMA piece (buffer_load_dwordx4 ... lds): voffset per lane, soffset scalar, the
+// LDS destination wave-uniform (M0). A device-only wrapper: the builtin in a kernel body would keep hipcc's
+// host pass from emitting the kernel's launch stub.
+F5H_DEV void dma16(__amdgpu_buffer_rsrc_t r, LDS_PTR(void) dst, uint32_t voff, uint32_t soff) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, dst, 16, voff, soff, 0, 0);
+}
 
 template <int B, int E, typename F>
 F5H_DEV void static_for(F&& f) {

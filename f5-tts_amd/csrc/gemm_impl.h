@@ -548,39 +548,46 @@ __global__ __launch_bounds__(64 * WGM * WGN, 2) void gemm_kernel(GemmArgs g) {
   const TC* A = reinterpret_cast<const TC*>(g.A);
   const TC* W = reinterpret_cast<const TC*>(g.W);
 
-  // per-lane DMA source offsets (elements), fixed across K-steps. The swizzle goes on the
-  // SOURCE chunk so that (wave-uniform LDS base + lane*16) lands on the swz128 image.
-  int64_t aoff[AR], boff[BR];
+  // LDS-DMA by buffer_load ... lds against per-block buffers (the block's A rows and W rows): a lane's byte
+  // offset in its panel is fixed across K-steps (voffset; the swizzle goes on the SOURCE chunk so that the
+  // wave-uniform LDS base + lane*16 lands on the swz128 image), the K-step's a scalar (soffset) and the LDS
+  // destination a scalar (M0), so a stage costs no vector instructions. Rows past M (N) are outside the
+  // buffer and read as zero; they feed only unstored outputs.
+  const int wid_s = __builtin_amdgcn_readfirstlane(wid);
+  constexpr int ESZ = (int)sizeof(TC);
+  const uint32_t abytes = (uint32_t)(min(BM, g.M - m0) * g.lda * ESZ);
+  const uint32_t wbytes = (uint32_t)(min(BN, g.N - n0) * g.ldw * ESZ);
+  uint32_t aoff[AR], boff[BR];
   static_for<0, AR>([&](auto I) {
     constexpr int i = decltype(I)::value;
     const int p = (i * NW + wid) * 64 + lane, row = p / CPR, slot = p % CPR;
-    const int m = min(m0 + row, g.M - 1);  // rows past M feed only unstored outputs
-    aoff[i] = (int64_t)m * g.lda + swz(row, slot) * E;
+    aoff[i] = (uint32_t)((row * g.lda + swz(row, slot) * E) * ESZ);
   });
   static_for<0, BR>([&](auto I) {
     constexpr int i = decltype(I)::value;
     const int p = (i * NW + wid) * 64 + lane, row = p / CPR, slot = p % CPR;
-    const int n = min(n0 + row, g.N - 1);  // likewise for weight rows past N
-    boff[i] = (int64_t)n * g.ldw + swz(row, slot) * E;
+    boff[i] = (uint32_t)((row * g.ldw + swz(row, slot) * E) * ESZ);
   });
   // A columns [k_split, K) come from the second panel A2 (cat(x, skip) of UNetT, unett.py:288-297):
   // a stage never straddles k_split (a multiple of the stage width)
   const TC* A2 = reinterpret_cast<const TC*>(g.A2);
+  const __amdgpu_buffer_rsrc_t wrs =
+      rsrc_of(W + (int64_t)n0 * g.ldw, wbytes);
   auto stage = [&](int buf, int k0) {
     uint4* As = lds + buf * stage_u4;
     uint4* Bs = As + BM * CPR;
     const bool second = A2 && k0 >= g.k_split;
     const TC* Ab = second ? A2 : A;
     const int ka = second ? k0 - g.k_split : k0;
+    const __amdgpu_buffer_rsrc_t ars =
+        rsrc_of(Ab + (int64_t)m0 * g.lda, abytes);
     static_for<0, AR>([&](auto I) {
       constexpr int i = decltype(I)::value;
-      __builtin_amdgcn_global_load_lds((const void*)(Ab + aoff[i] + ka), (LDS_PTR(void))(As + (i * NW + wid) * 64),
-                                       16, 0, 0);
+      dma16(ars, (LDS_PTR(void))(As + (i * NW + wid_s) * 64), aoff[i], ka * ESZ);
     });
     static_for<0, BR>([&](auto I) {
       constexpr int i = decltype(I)::value;
-      __builtin_amdgcn_global_load_lds((const void*)(W + boff[i] + k0), (LDS_PTR(void))(Bs + (i * NW + wid) * 64),
-                                       16, 0, 0);
+      dma16(wrs, (LDS_PTR(void))(Bs + (i * NW + wid_s) * 64), boff[i], k0 * ESZ);
     });
   };
 
@@ -821,22 +828,20 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(GemmArgs g) {
   // rows (i*4 + w4)*16 .. +15 of its operand; lane -> (row = lane>>2, physical chunk lane&3).
   constexpr int NI = NA > NB ? NA : NB;
   const int nI = grp == 0 ? NA : NB;
-  const TC* src[NI];
-  const TC* src2[NI];  // A rows in the second A panel (g.A2: columns [k_split, K)), group 0 only
-  uint32_t dst_off[NI];
+  // by buffer_load ... lds against the group's panel (its A rows or W rows): the lane's byte offset is fixed,
+  // the stage's K offset a scalar (soffset), so a stage costs no vector instructions; rows past M (N) read as
+  // zero and feed only unstored outputs
+  const int ld = grp == 0 ? g.lda : g.ldw;
+  const TC* pan = grp == 0 ? A + (int64_t)m0 * g.lda : W + (int64_t)n0 * g.ldw;
+  const TC* pan2 = (grp == 0 && g.A2) ? reinterpret_cast<const TC*>(g.A2) + (int64_t)m0 * g.lda : pan;
+  const uint32_t pbytes = (uint32_t)((grp == 0 ? min(BM, g.M - m0) : min(BN, g.N - n0)) * ld * 2);
+  uint32_t voff[NI], dst_off[NI];
 #pragma unroll
   for (int i = 0; i < NI; ++i) {
     const int row = (i * 4 + w4) * 16 + (lane >> 2);
     const int lc = swz64(row, lane & 3);  // logical chunk held at this physical slot
-    if (grp == 0) {
-      src[i] = A + (int64_t)min(m0 + row, g.M - 1) * g.lda + lc * 8;
-      src2[i] = g.A2 ? reinterpret_cast<const TC*>(g.A2) + (int64_t)min(m0 + row, g.M - 1) * g.lda + lc * 8 : src[i];
-      dst_off[i] = (uint32_t)((i * 4 + w4) * 16 * 64);
-    } else {
-      src[i] = W + (int64_t)min(n0 + row, g.N - 1) * g.ldw + lc * 8;
-      src2[i] = src[i];
-      dst_off[i] = (uint32_t)(BM * 64 + (i * 4 + w4) * 16 * 64);
-    }
+    voff[i] = (uint32_t)((row * ld + lc * 8) * 2);
+    dst_off[i] = (uint32_t)((grp == 0 ? 0 : BM * 64) + (i * 4 + w4) * 16 * 64);
   }
   char* lds_c = reinterpret_cast<char*>(lds);
   auto dma_phase = [&](int p) {  // this wave's part of phase p (KS stages)
@@ -844,12 +849,14 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(GemmArgs g) {
 #pragma unroll
     for (int s = 0; s < KS; ++s) {
       const int k0 = (p * KS + s) * 32;
-      const bool second = grp == 0 && g.A2 && k0 >= g.k_split;
+      const bool second = grp == 0 && g.A2 && k0 >= g.k_split;  // A columns [k_split, K) from the A2 panel
+      const __amdgpu_buffer_rsrc_t rs =
+          rsrc_of(second ? pan2 : pan, pbytes);
+      const int ks = second ? k0 - g.k_split : k0;
 #pragma unroll
       for (int i = 0; i < NI; ++i)
         if (i < nI)
-          __builtin_amdgcn_global_load_lds((const void*)(second ? src2[i] + (k0 - g.k_split) : src[i] + k0),
-                                           (LDS_PTR(void))(lds_c + slot * PB + s * SB + dst_off[i]), 16, 0, 0);
+          dma16(rs, (LDS_PTR(void))(lds_c + slot * PB + s * SB + dst_off[i]), voff[i], ks * 2);
     }
   };
   // own DMA of phase `need` landed, given phases up to `issued` were issued (counted vmcnt:
@@ -1022,33 +1029,35 @@ __global__ __launch_bounds__(512, 1) void gemm_8p_kernel(GemmArgs g) {
 
   // ---- DMA sources: thread tid fills chunks p = j*512 + tid (j = 0, 1) of each half: row p >> 3, slot p & 7,
   // holding the global chunk swz128g(row, slot) (an involution: the reader XORs the same way)
-  int64_t soff[4][2];
+  // by buffer_load ... lds against the block's A and W panels (byte offsets per lane fixed, the K-tile's a
+  // scalar soffset: no vector instructions per half-tile); rows past M (N) read as zero (unstored outputs)
+  uint32_t voff[4][2];
 #pragma unroll
   for (int h = 0; h < 4; ++h)
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
       const int p = j * 512 + tid, row = p >> 3, slot = p & 7;
       const int chunk = swz128g(row, slot);
-      if (h < 2) {
-        const int m = min(m0 + h * 128 + row, g.M - 1);  // rows past M feed only unstored outputs
-        soff[h][j] = (int64_t)m * g.lda + chunk * 8;
-      } else {
-        const int n = min(n0 + (h - 2) * 128 + row, g.N - 1);
-        soff[h][j] = (int64_t)n * g.ldw + chunk * 8;
-      }
+      voff[h][j] = (uint32_t)((((h & 1) * 128 + row) * (h < 2 ? g.lda : g.ldw) + chunk * 8) * 2);
     }
+  const uint32_t abytes = (uint32_t)(min(256, g.M - m0) * g.lda * 2), wbytes = (uint32_t)(min(256, g.N - n0) * g.ldw * 2);
+  const __amdgpu_buffer_rsrc_t wrs =
+      rsrc_of(W + (int64_t)n0 * g.ldw, wbytes);
   char* lds_c = reinterpret_cast<char*>(lds);
   auto dma_half = [&](int t, int h) {  // half h (0 A-top, 1 A-bottom, 2 B-left, 3 B-right) of K-tile t
     const int k0 = t * KT;
     char* dst = lds_c + (t & 1) * BUF + h * HALF + wid * 64 * 16;
+    if (h < 2) {
+      const bool second = A2 && k0 >= g.k_split;
+      const __amdgpu_buffer_rsrc_t ars = rsrc_of((second ? A2 : A) + (int64_t)m0 * g.lda, abytes);
+      const int ka = second ? k0 - g.k_split : k0;
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const TC* src;
-      if (h < 2)
-        src = (A2 && k0 >= g.k_split) ? A2 + soff[h][j] + (k0 - g.k_split) : A + soff[h][j] + k0;
-      else
-        src = W + soff[h][j] + k0;
-      __builtin_amdgcn_global_load_lds((const void*)src, (LDS_PTR(void))(dst + j * 512 * 16), 16, 0, 0);
+      for (int j = 0; j < 2; ++j)
+        dma16(ars, (LDS_PTR(void))(dst + j * 512 * 16), voff[h][j], ka * 2);
+    } else {
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+        dma16(wrs, (LDS_PTR(void))(dst + j * 512 * 16), voff[h][j], k0 * 2);
     }
   };
 
