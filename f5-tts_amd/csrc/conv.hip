@@ -150,6 +150,9 @@ __global__ __launch_bounds__(128 * NWM, 1) void conv_kernel(ConvArgs a) {
   constexpr int NWV = NT / 64;              // waves
   constexpr int WR = 64 * CPR / NT;         // DMA rounds per tap (64 rows x CPR chunks / NT lanes)
   static_assert(WR >= 1 && WR * NT == 64 * CPR, "whole DMA rounds per tap");
+  // by buffer_load ... lds over the group's tap panel: lane offset fixed, the tap's a scalar, M0 wave-uniform
+  const int wid_s = __builtin_amdgcn_readfirstlane(wid);
+  const __amdgpu_buffer_rsrc_t wrs = rsrc_of(Wg, (uint64_t)31 * 64 * 64 * sizeof(TC));
   int woff[WR];
   static_for<0, WR>([&](auto I) {
     constexpr int r = decltype(I)::value;
@@ -165,8 +168,8 @@ __global__ __launch_bounds__(128 * NWM, 1) void conv_kernel(ConvArgs a) {
         uint4* Ws = Ws0 + (buf * TS + u) * 64 * CPR;
         static_for<0, WR>([&](auto I) {
           constexpr int r = decltype(I)::value;
-          __builtin_amdgcn_global_load_lds((const void*)(Wg + (int64_t)t * 64 * 64 + woff[r]),
-                                           (LDS_PTR(void))(Ws + (r * NWV + wid) * 64), 16, 0, 0);
+          dma16(wrs, (LDS_PTR(void))(Ws + (r * NWV + wid_s) * 64), (uint32_t)(woff[r] * (int)sizeof(TC)),
+                (uint32_t)(t * 64 * 64 * (int)sizeof(TC)));
         });
       }
     });
@@ -316,14 +319,17 @@ __global__ __launch_bounds__(512, 1) void conv16_kernel(ConvArgs a) {
   // tap panel: lane chunk p = wid*64 + lane -> row p/8, source chunk swz_tap(row, p%8) (involution)
   const int prow = (wid * 64 + lane) / CPR, pslot = (wid * 64 + lane) % CPR;
   const int woff = prow * 64 + swz_tap(prow, pslot) * 8;
+  // by buffer_load ... lds over the group's tap panel: lane offset fixed, the tap's a scalar, M0 wave-uniform
+  const int wid_s = __builtin_amdgcn_readfirstlane(wid);
+  const __amdgpu_buffer_rsrc_t wrs = rsrc_of(Wg, (uint64_t)31 * 64 * 64 * sizeof(TC));
   auto wdma = [&](int st) {  // stage st -> ring slot st % RING; one 1 KB piece per tap per wave
     uint4* Wslot = Ws0 + (st % RING) * TS * TAPB;
 #pragma unroll
     for (int u = 0; u < TS; ++u) {
       const int t = st * TS + u;
       if (t < 31)
-        __builtin_amdgcn_global_load_lds((const void*)(Wg + (int64_t)t * 64 * 64 + woff),
-                                         (LDS_PTR(void))(Wslot + u * TAPB + wid * 64), 16, 0, 0);
+        dma16(wrs, (LDS_PTR(void))(Wslot + u * TAPB + wid_s * 64), (uint32_t)(woff * (int)sizeof(TC)),
+              (uint32_t)(t * 64 * 64 * (int)sizeof(TC)));
     }
   };
   auto taps_of = [](int st) { return st < 0 || st >= NST ? 0 : (31 - st * TS < TS ? 31 - st * TS : TS); };
