@@ -361,16 +361,36 @@ F5H_DEV void epilogue_fast_t(const GemmArgs& g, const f32x4 (&acc)[MT][NT], floa
   };
   const __amdgpu_buffer_rsrc_t rk = rsrc_of(g.rowkeep, g.rowkeep ? (uint64_t)g.M : 0);  // null: reads 0
   const bool masked = g.rowkeep != nullptr;
+  // QKV: (sequence, position) of each of the lane's chunk rows, for the strip being fetched (pf) and the one being
+  // stored (ps), advanced by 16 rows per strip (one division per chunk row for the whole epilogue, not two per
+  // strip). Rows past M get positions too: the RoPE table index stays in range and their stores are dropped.
+  int pf_sq[TPC], pf_pos[TPC], ps_sq[TPC], ps_pos[TPC];
+  if constexpr (EPI == EPI_QKV) {
+#pragma unroll
+    for (int t = 0; t < TPC; ++t) {
+      const int row0 = rbase + t * (64 / CH) + lane / CH;
+      pf_sq[t] = ps_sq[t] = fdiv(row0, g.seq_len);
+      pf_pos[t] = ps_pos[t] = row0 - pf_sq[t] * g.seq_len;
+    }
+  }
+  auto advance = [&](int& sq, int& pos) {
+    pos += 16;
+    while (pos >= g.seq_len) {
+      pos -= g.seq_len;
+      ++sq;
+    }
+  };
   auto fetch = [&](int i, RowIn (&ri)[TPC]) {
 #pragma unroll
     for (int t = 0; t < TPC; ++t) {
       const int rr = t * (64 / CH) + lane / CH;
       const int rowc = min(rbase + i * 16 + rr, g.M - 1);
       if constexpr (EPI == EPI_QKV) {
-        const int pos = rowc - fdiv(rowc, g.seq_len) * g.seq_len;
-        const u32x4* p = reinterpret_cast<const u32x4*>(g.rope + (int64_t)pos * 32 + (dh >> 1));
+        (void)rowc;
+        const u32x4* p = reinterpret_cast<const u32x4*>(g.rope + pf_pos[t] * 32 + (dh >> 1));
         ri[t].d0 = p[0];
         ri[t].d1 = p[1];
+        advance(pf_sq[t], pf_pos[t]);
       } else if constexpr (EPI == EPI_RESID || EPI == EPI_RESID16) {
         if constexpr (!PREF) {
           const u32x4* p = reinterpret_cast<const u32x4*>(reinterpret_cast<const ResT<TC, EPI>*>(
@@ -444,8 +464,9 @@ F5H_DEV void epilogue_fast_t(const GemmArgs& g, const f32x4 (&acc)[MT][NT], floa
           x.v[2 * p] = r.x;
           x.v[2 * p + 1] = r.y;
         }
-        const int sq = fdiv(row, g.seq_len), pos = row - sq * g.seq_len;
-        store8_rs<TC>(dst, (uint32_t)((((int64_t)sq * g.heads + head) * g.seq_len + pos) * 64 + dh), x);
+        (void)row;
+        store8_rs<TC>(dst, (uint32_t)(((ps_sq[t] * g.heads + head) * g.seq_len + ps_pos[t]) * 64 + dh), x);
+        advance(ps_sq[t], ps_pos[t]);
       } else if constexpr (EPI == EPI_RESID || EPI == EPI_RESID16) {
         V8 c;
         if constexpr (PREF)
