@@ -276,6 +276,44 @@ __global__ __launch_bounds__(256) void rms_kernel(const TI* h, int M, int d, con
                  v[k].z / nrm * f * a[k].z, v[k].w / nrm * f * a[k].w);
   }
 }
+// 16-bit residual stream at d = 1024: 16-byte row accesses, lane l holding elements 8(l + 64k) .. +7 (k < 2)
+template <typename T>
+__global__ __launch_bounds__(256) void rms16_kernel(const T* h, int M, const float* g, T* out) {
+  typedef typename Op16<T>::v8 v8;
+  constexpr int d = 1024;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (row >= M) return;
+  const uint4* x = reinterpret_cast<const uint4*>(h + (int64_t)row * d);
+  const float4* gg = reinterpret_cast<const float4*>(g);
+  float v[2][8];
+  float4 a[2][2];
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const int c = lane + 64 * k;
+    const v8 w = __builtin_bit_cast(v8, x[c]);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[k][e] = to_f32(w[e]);
+    a[k][0] = gg[2 * c];
+    a[k][1] = gg[2 * c + 1];
+  }
+  float q = 0.f;
+#pragma unroll
+  for (int k = 0; k < 2; ++k)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) q += v[k][e] * v[k][e];
+  const float nrm = fmaxf(sqrtf(wave_sum_dpp(q)), 1e-12f);
+  const float f = sqrtf((float)d);
+  uint4* o = reinterpret_cast<uint4*>(out + (int64_t)row * d);
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const float av[8] = {a[k][0].x, a[k][0].y, a[k][0].z, a[k][0].w, a[k][1].x, a[k][1].y, a[k][1].z, a[k][1].w};
+    v8 w;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) w[e] = from_f32<T>(v[k][e] / nrm * f * av[e]);
+    o[lane + 64 * k] = __builtin_bit_cast(uint4, w);
+  }
+}
+
 hipError_t rms_norm_g(int compute, const void* hv, int h16, int M, int d, const float* g, void* out, hipStream_t st) {
   if (d % 4 || d > 4 * 64 * MAXV) return hipErrorInvalidValue;
   const dim3 gr(nblk(M, 4)), b(256);
@@ -285,7 +323,7 @@ hipError_t rms_norm_g(int compute, const void* hv, int h16, int M, int d, const 
       typedef decltype(tag) T;
       const T* x = (const T*)hv;
       switch (d) {
-        case 1024: hipLaunchKernelGGL((rms_kernel<T, 4, T>), gr, b, 0, st, x, M, d, g, (T*)out); break;
+        case 1024: hipLaunchKernelGGL((rms16_kernel<T>), gr, b, 0, st, x, M, g, (T*)out); break;
         case 512: hipLaunchKernelGGL((rms_kernel<T, 2, T>), gr, b, 0, st, x, M, d, g, (T*)out); break;
         default: hipLaunchKernelGGL((rms_kernel<T, 0, T>), gr, b, 0, st, x, M, d, g, (T*)out);
       }
