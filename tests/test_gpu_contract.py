@@ -461,10 +461,12 @@ def test_engine_drop_never_waits_for_other_streams():
     finally:
         for n in names:
             setattr(L, n, orig[n])
+    # another stream's launch is not held up on the host (a hipFree in the release would block every HIP call
+    # of the process until the spin ends). Only the enqueue is timed: with GPU_MAX_HW_QUEUES streams share
+    # hardware queues, so the kernel itself may queue behind the spin; its result is checked afterwards.
     t0 = time.perf_counter()
     with torch.cuda.stream(third):
         y = x * 2.0
-    third.synchronize()
     third_op = time.perf_counter() - t0
     t0 = time.perf_counter()
     still_busy = not other.query()
@@ -477,6 +479,7 @@ def test_engine_drop_never_waits_for_other_streams():
     assert max(max(v) for v in calls.values()) < 0.05, calls  # each release returns at once
     assert took < 0.5, took  # the whole drop (collector included) does not wait for the 1 s spin
     assert third_op < 0.05 and query < 0.05, (third_op, query)
+    third.synchronize()
     assert torch.equal(y, x * 2.0)
     _lib.lib().f5h_release_pending(1)  # returns once the releases ran (after the spin, on the reaper)
     assert _lib.lib().f5h_release_pending(0) == 0
