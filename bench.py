@@ -317,18 +317,24 @@ def class_entry(kc, avg_ms, n, arch, S, L, launches_per_call, ms_call, chains=1,
     if traffic and kc in ("qkv", "out", "ffn1", "ffn2", "attention", "conv"):
         d, ff = arch["dim"], int(arch["dim"] * arch["ff_mult"])
         kn = {"qkv": (d, 3 * d), "out": (d, d), "ffn1": (d, ff), "ffn2": (ff, d)}.get(kc)
+        # rows the launch must touch: with the pad-row skip (live pricing) the out-projection's live rows only
+        rows = sum(qlens) if (padded is not None and kc == "out") else S * L
         if kn:  # operands + result at the operand width (residual read+write for RESID)
             K, Nn = kn
-            alg = esz * (S * L * K + Nn * K) + (2 * resid_bytes(arch, esz) if kc in ("out", "ffn2") else esz) * S * L * Nn
+            alg = esz * (rows * K + Nn * K) + (2 * resid_bytes(arch, esz) if kc in ("out", "ffn2") else esz) * rows * Nn
         elif kc == "conv":  # the mean of the two grouped conv layers (tools/pmc_classes.py): layer 1 reads the
             # fp32 input embedding and writes the operand dtype, layer 2 reads that, the fp32 input embedding
             # (its residual) and writes the residual stream; plus the 16 groups' 31-tap weights
             per_elem = ((4 + esz) + (esz + 4 + resid_bytes(arch, esz))) / 2
             alg = S * L * d * per_elem + d * (d // 16) * 31 * esz
+        elif padded is not None:  # K and V of every row, Q read and O written for the live query rows only
+            alg = 2 * esz * arch["heads"] * 64 * (S * L + sum(qlens))
         else:
-            alg = 4 * 2 * S * arch["heads"] * L * 64
+            alg = 4 * esz * S * arch["heads"] * L * 64
         e["algorithmic_bytes"] = alg
         e["traffic_over_algorithmic"] = round(traffic / alg, 3)
+    elif traffic and e.get("bytes_per_launch"):  # an HBM-bound class: against the bytes it is priced on
+        e["traffic_over_algorithmic"] = round(traffic / e["bytes_per_launch"], 3)
     return e
 
 

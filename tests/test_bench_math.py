@@ -51,13 +51,21 @@ def test_norm_bytes_follow_the_residual_width():
 
 
 def test_pmc_traffic_only_at_the_measured_shape():
-    """The committed PMC summary is attached to a bench line only at the launch shape it was measured
-    on (C2: S=2, N=1876, Base); any other shape (C3, C5, fp32 tiny) reports no traffic."""
+    """A committed PMC summary is attached to a bench line only at the launch shape it was measured on
+    (C2: S=2, N=1876, Base; C3/C4: S=64 and the workload named; C5: S=16, N=1877, UNetT depth 24); any
+    other shape or workload reports no traffic."""
     c2 = {"S": 2, "L": 1876, "dim": 1024, "depth": 22}
     t, src = bench.pmc_traffic("attention", c2)
     assert t and t > 0 and src.startswith("profiles/")
-    t, src = bench.pmc_traffic("attention", dict(c2, S=64))
+    t, src = bench.pmc_traffic("attention", dict(c2, S=8))
     assert t is None and "no profiles" in src
+    t3, src3 = bench.pmc_traffic("qkv", dict(c2, S=64, config="c3"))
+    t4, src4 = bench.pmc_traffic("qkv", dict(c2, S=64, config="c4"))
+    assert "c3" in src3 and "c4" in src4 and t3 != t4
+    t, src = bench.pmc_traffic("qkv", dict(c2, S=64, config="c9"))
+    assert t is None and "no profiles" in src
+    t, src = bench.pmc_traffic("ffn1", {"S": 16, "L": 1877, "dim": 1024, "depth": 24, "config": "c5"})
+    assert t and "c5" in src
 
 
 def test_timing_summaries_only_for_the_measured_compute_type():
@@ -173,3 +181,19 @@ def test_pad_skip_prices_attention_and_out_on_live_rows():
     assert f["flops_per_launch"] == bench.class_flops("ffn1", arch, S, L) and "padded_flops_per_launch" not in f
     same = bench.class_entry("attention", 1.0, 8, arch, S, L, 22, 100.0, qlens=[L] * S)
     assert same["flops_per_launch"] == bench.class_flops("attention", arch, S, L)
+
+
+def test_live_row_traffic_pricing_at_c3():
+    """With the pad-row skip (ragged C3 batch) attention reads K and V of every row but Q and O of the live
+    query rows only, and the out-projection touches live rows only: their algorithmic bytes count those rows,
+    so the measured traffic of the committed C3 PMC summary is >= ~1x of them (it was 0.86x / 0.95x of the
+    padded count)."""
+    arch = configs.get_arch("F5TTS_v1_Base")
+    tot = [564 + (i * 1312) // 31 for i in range(32)]
+    q = tot * 2  # CFG copies
+    at = bench.class_entry("attention", 1.058, 8, arch, 64, 1876, 704, 2262.0, 1, config="c3", qlens=q)
+    assert at["algorithmic_bytes"] == 2 * 2 * 16 * 64 * (64 * 1876 + sum(q))
+    out = bench.class_entry("out", 0.300, 8, arch, 64, 1876, 704, 2262.0, 1, config="c3", qlens=q)
+    assert out["algorithmic_bytes"] == 2 * (sum(q) * 1024 + 1024 * 1024) + 2 * 2 * sum(q) * 1024
+    for e in (at, out):
+        assert e["traffic"] and 0.95 < e["traffic_over_algorithmic"] < 2.0

@@ -33,11 +33,9 @@ import statistics
 import sys
 from collections import defaultdict
 
-from pmc_classes import classify
+from pmc_classes import SHAPES as _SHAPES, classify
 
-SHAPES = {"c2": {"config": "c2", "S": 2, "L": 1876, "dim": 1024, "depth": 22},
-          "c3": {"config": "c3", "S": 64, "L": 1876, "dim": 1024, "depth": 22},
-          "c4": {"config": "c4", "S": 64, "L": 1876, "dim": 1024, "depth": 22}}
+SHAPES = {c: {k: s[k] for k in ("config", "S", "L", "dim", "depth")} for c, s in _SHAPES.items()}
 NSIMD = 1024  # 256 CUs x 4 SIMDs
 
 
