@@ -386,6 +386,21 @@ def _free_port():
     return port
 
 
+def visible_gpus():
+    """GPUs a rank process would see, counted in a child process: the launcher's own process makes no HIP
+    call at all (torch.cuda.device_count() can fall back to hipGetDeviceCount when amdsmi cannot initialise,
+    which starts the HIP runtime in the parent of the ranks)."""
+    import subprocess
+
+    code = "import torch; print(torch.cuda.device_count())"
+    try:
+        out = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=300,
+                             env=dict(os.environ))
+        return int(out.stdout.strip().splitlines()[-1])
+    except (subprocess.SubprocessError, ValueError, IndexError):
+        return 0
+
+
 def launch_ranks(args, argv):
     """`--gpus N` with no outer launcher: start N fresh rank processes of this script, one per GPU, with
     RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR / MASTER_PORT set (what torchrun would set; the reference's
@@ -396,7 +411,7 @@ def launch_ranks(args, argv):
 
     n = args.gpus
     if not args.standin:
-        have = torch.cuda.device_count()  # does not initialise the GPU (HIP runtime not started)
+        have = visible_gpus()
         if have < n:
             print(f"bench.py: --gpus {n} but only {have} GPU(s) visible", file=sys.stderr)
             return 2

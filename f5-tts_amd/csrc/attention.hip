@@ -107,12 +107,13 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn16_kernel(AttnArgs a) {
   const int qrow = qb * (32 * NW) + wid * 32 + (lane & 31);
 
   // ---- LDS-DMA of a K/V tile: chunk p = (r*NW + w)*64 + lane of the 64-row x 8-chunk image, by
-  // buffer_load ... lds: the lane's byte offset in the tile is fixed (voffset), the tile's is a scalar
-  // (soffset), the LDS destination a scalar (M0), so a tile's DMA costs no vector instructions; rows past L
-  // are outside the buffer and read as zero (their keys are masked, their P is 0)
+  // buffer_load ... lds: the lane's byte offset in the tile is fixed (voffset), the LDS destination a scalar
+  // (M0), so a tile's DMA costs no vector instructions. Each tile gets its own descriptor (scalar base at the
+  // tile's first key, extent = the tile's keys below L): the range check then covers every row past L from
+  // voffset alone, whatever the hardware does with soffset (an extent over the whole [L,64] panel with the tile
+  // offset in soffset would let the ragged last tile read the next (sequence, head)'s rows, or past V). Rows
+  // past L read as zero; their keys are masked and their P is 0, so no stale NaN can reach the P.V MFMA.
   const int wid_s = __builtin_amdgcn_readfirstlane(wid);
-  const __amdgpu_buffer_rsrc_t krs = rsrc_of(K, L * 128);
-  const __amdgpu_buffer_rsrc_t vrs = rsrc_of(V, L * 128);
   uint32_t dvoff[CPW];
 #pragma unroll
   for (int r = 0; r < CPW; ++r) {
@@ -122,10 +123,13 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn16_kernel(AttnArgs a) {
   auto dma = [&](int buf, int kt) {
     uint4* Ks = lds + buf * (TILE_B / 16);
     uint4* Vs = Ks + 512;
+    const uint32_t ext = (uint32_t)max(0, min(64, L - kt * 64)) * 128u;
+    const __amdgpu_buffer_rsrc_t krs = rsrc_of(K + (int64_t)kt * 4096, ext);
+    const __amdgpu_buffer_rsrc_t vrs = rsrc_of(V + (int64_t)kt * 4096, ext);
 #pragma unroll
     for (int r = 0; r < CPW; ++r) {
-      dma16(krs, (LDS_PTR(void))(Ks + (r * NW + wid_s) * 64), dvoff[r], kt * 8192);
-      dma16(vrs, (LDS_PTR(void))(Vs + (r * NW + wid_s) * 64), dvoff[r], kt * 8192);
+      dma16(krs, (LDS_PTR(void))(Ks + (r * NW + wid_s) * 64), dvoff[r], 0);
+      dma16(vrs, (LDS_PTR(void))(Vs + (r * NW + wid_s) * 64), dvoff[r], 0);
     }
   };
 

@@ -935,6 +935,19 @@ int f5h_engine_create_views(const f5h_arch* arch, const f5h_tensor_view* weights
   if (const char* gv = getenv("F5H_GRAPH")) e->graph_mode = atoi(gv) ? 1 : 0;
   if (const char* sv = getenv("F5H_SPLIT_CFG")) e->split_cfg = std::min(2, std::max(0, atoi(sv)));
   if (const char* pv = getenv("F5H_NO_PAD_SKIP")) e->pad_skip = (*pv == '1') ? 0 : 1;
+  // device views are read on the engine's non-blocking stream: order it behind the null stream (so behind
+  // every blocking stream's queued work, the ordering the packing had when it ran on the null stream); work
+  // on other non-blocking streams must be complete (f5h.h)
+  {
+    hipEvent_t ev = nullptr;
+    if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) == hipSuccess) {
+      if (hipEventRecord(ev, nullptr) != hipSuccess || hipStreamWaitEvent(e->mstream, ev, 0) != hipSuccess)
+        (void)hipGetLastError();
+      (void)hipEventDestroy(ev);
+    } else {
+      (void)hipGetLastError();
+    }
+  }
   // host views: staged once, in their own dtype, into temporaries freed after packing
   WMap W;
   std::vector<void*> staged;
@@ -1555,6 +1568,11 @@ int f5h_gemm_force_config(int32_t cfg) {
   gemm_force_config(cfg);
   g_kernel_epoch.fetch_add(1);
   return 0;
+}
+
+int f5h_debug_tile_live(const int32_t* live_len, int32_t live_seq, int32_t M, int32_t m0, int32_t BM) {
+  if (live_seq <= 0 || M <= 0 || BM <= 0 || m0 < 0 || m0 >= M) return fail(F5H_EINVAL, "bad tile");
+  return tile_live_rows(live_len, live_seq, M, m0, BM) ? 1 : 0;
 }
 
 int f5h_op_attention(void* stream, int32_t compute, int32_t S, int32_t H, int32_t N, const float* Q, const float* K,

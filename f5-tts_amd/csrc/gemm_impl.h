@@ -136,14 +136,9 @@ F5H_DEV int fdiv(int n, int d) {
 }
 
 // Does the row tile [m0, m0 + BM) hold a live row (GemmArgs::live_len)? Wave-uniform (scalar loads).
+// (tile_live_rows: kernels.h, host-callable too: f5h_debug_tile_live and tests/test_host.py check it)
 F5H_DEV bool tile_live(const GemmArgs& g, int m0, int BM) {
-  if (!g.live_len) return true;
-  const int last = min(m0 + BM, g.M) - 1;
-  for (int s = m0 / g.live_seq; s <= last / g.live_seq; ++s) {
-    const int r0 = s * g.live_seq;
-    if (m0 < r0 + g.live_len[s]) return true;  // the tile starts before sequence s's live rows end
-  }
-  return false;
+  return tile_live_rows(g.live_len, g.live_seq, g.M, m0, BM);
 }
 
 // Apply the epilogue to 8 consecutive columns [col, col+8) of output row `row`.

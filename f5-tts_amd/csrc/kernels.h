@@ -67,6 +67,22 @@ struct GemmArgs {
   const int32_t* live_len; int live_seq;
 };
 
+// Does the row tile [m0, m0 + BM) of an M-row GEMM hold a live row? Sequence s (rows [s*live_seq, (s+1)*live_seq))
+// contributes the tile's rows [max(m0, r0), min(last + 1, r0 + live_seq)); its live rows are [r0, r0 +
+// live_len[s]): the tile is live iff one of those overlaps is non-empty. Null live_len: always live. Host and
+// device (the GEMM kernels' pad-row skip; f5h_debug_tile_live checks it from the CPU tests).
+__host__ __device__ inline bool tile_live_rows(const int32_t* live_len, int live_seq, int M, int m0, int BM) {
+  if (!live_len) return true;
+  const int last = (m0 + BM < M ? m0 + BM : M) - 1;
+  for (int s = m0 / live_seq; s <= last / live_seq; ++s) {
+    const int r0 = s * live_seq;
+    const int lo = m0 > r0 ? m0 : r0;
+    const int hi_tile = last + 1, hi_live = r0 + live_len[s];
+    if (lo < (hi_tile < hi_live ? hi_tile : hi_live)) return true;
+  }
+  return false;
+}
+
 // compute: ComputeMode (fp32 / bf16 / fp16 operands). A and W both in the operand dtype.
 hipError_t gemm(int compute, int epi, const GemmArgs& a, hipStream_t st);
 // pin the 16-bit GEMM tile configuration (0, 1, 5, 11; -1 = automatic choice); tuning and test hook

@@ -17,7 +17,23 @@ void UseLog::note(hipStream_t st) {
   for (auto& p : ev)
     if (p.first == st) e = p.second;
   if (!e) {
-    if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) {
+    // a new stream: first drop the entries whose last use has completed (a caller that makes a stream per
+    // request would otherwise grow the list, and this scan, for the object's lifetime); one completed event
+    // is reused for the new stream instead of creating one
+    for (size_t i = 0; i < ev.size();) {
+      if (hipEventQuery(ev[i].second) == hipSuccess) {
+        if (!e)
+          e = ev[i].second;
+        else
+          (void)hipEventDestroy(ev[i].second);
+        ev[i] = ev.back();
+        ev.pop_back();
+      } else {
+        (void)hipGetLastError();  // hipErrorNotReady
+        ++i;
+      }
+    }
+    if (!e && hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) {
       (void)hipGetLastError();
       return;
     }
@@ -52,7 +68,12 @@ hipMemPool_t pool_of(int dev) {
     (void)hipGetLastError();
     return nullptr;
   }
-  uint64_t keep = ~0ull;  // never trimmed implicitly (a trim at a synchronisation point would free memory)
+  // Default: never trimmed implicitly (a trim at a synchronisation point frees memory, and that waits for the
+  // device). Released memory then stays reserved for this process's next engine / Vocos / log-mel object:
+  // f5h_release_pending(2) (Python: f5_tts_amd.release_memory()) returns it; F5H_POOL_KEEP_MB=<n> caps what
+  // the pool keeps past a synchronisation point instead (memory).
+  uint64_t keep = ~0ull;
+  if (const char* kv = getenv("F5H_POOL_KEEP_MB")) keep = (uint64_t)strtoull(kv, nullptr, 10) << 20;
   (void)hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &keep);
   g_pools.emplace_back(dev, pool);
   return pool;

@@ -6,3 +6,11 @@ the reference's Python surface (`f5_tts.model.{CFM, DiT, UNetT}`, `f5_tts.api.F5
 """
 
 __version__ = "0.1.0"
+
+
+def release_memory() -> int:
+    """Wait for queued engine / Vocos / log-mel releases, then return the device pool's unused memory to the
+    system (f5h_release_pending(2); waits for the device). Returns the releases still pending (0)."""
+    from . import _lib
+
+    return int(_lib.lib().f5h_release_pending(2))

@@ -42,6 +42,7 @@ EXPORTS = (
     "f5h_op_linear",
     "f5h_op_attention",
     "f5h_gemm_force_config",
+    "f5h_debug_tile_live",
     "f5h_vocos_create",
     "f5h_vocos_destroy",
     "f5h_vocos_workspace_size",
@@ -155,6 +156,8 @@ def lib():
     L.f5h_op_attention.restype = ctypes.c_int
     L.f5h_gemm_force_config.argtypes = [i32]
     L.f5h_gemm_force_config.restype = ctypes.c_int
+    L.f5h_debug_tile_live.argtypes = [vp, i32, i32, i32, i32]
+    L.f5h_debug_tile_live.restype = ctypes.c_int
     L.f5h_vocos_create.argtypes = [ctypes.POINTER(VocosArch), ctypes.POINTER(Weight), i32, i32, ctypes.POINTER(vp)]
     L.f5h_vocos_create.restype = ctypes.c_int
     L.f5h_vocos_destroy.argtypes = [vp]

@@ -256,12 +256,16 @@ def op_linear(A, W, bias=None, compute="bf16"):
     return C
 
 
-def op_attention(Q, K, V, kv_len=None, compute="bf16", q_prescaled=False):
-    """O[S,N,H*64] = softmax(Q K^T/8) V; q_prescaled: Q already carries (1/8)*log2(e)."""
+def op_attention(Q, K, V, kv_len=None, compute="bf16", q_prescaled=False, poison=False):
+    """O[S,N,H*64] = softmax(Q K^T/8) V; q_prescaled: Q already carries (1/8)*log2(e). poison: fill the
+    workspace (16-bit q | k | v | o, back to back) with NaN bits first, so a kernel that reads key rows past N
+    (the next (sequence, head)'s rows, or past V into O) turns its output NaN."""
     S, H, N, D = Q.shape
     assert D == 64
     O = torch.empty(S, N, H * 64, dtype=torch.float32, device=Q.device)
     ws = torch.empty(Q.numel() * 8 + 1024, dtype=torch.uint8, device=Q.device)
+    if poison:
+        ws.fill_(0xFF)
     kv = None if kv_len is None else kv_len.to(Q.device, torch.int32).contiguous()
     _lib.check(_lib.lib().f5h_op_attention(_lib.stream_handle(Q.device), _lib.COMPUTE[compute], S, H, N,
                                            Q.contiguous().data_ptr(), K.contiguous().data_ptr(),

@@ -94,7 +94,9 @@ typedef struct f5h_engine f5h_engine;
  * weights into the engine's device layout (bf16/fp16/fp32 GEMM panels, conv taps, the
  * concatenated AdaLN matrix). Host views are staged to the device in their own dtype; every
  * panel is packed on the device (no host fp32 copy of the model). Blocks until packing is complete;
- * the views may be released afterwards. */
+ * the views may be released afterwards. Device views are read on the engine's own non-blocking stream,
+ * ordered behind the null stream (hence behind work queued on blocking streams): the caller must have
+ * completed any write to them still queued on a non-blocking stream (e.g. a torch side stream). */
 int f5h_engine_create_views(const f5h_arch* arch, const f5h_tensor_view* weights, int32_t n_weights,
                             int32_t device, f5h_engine** out);
 /* The same from fp32 host arrays (f5h_weight). */
@@ -226,6 +228,11 @@ int f5h_op_attention(void* stream, int32_t compute, int32_t S, int32_t H, int32_
 /* Tuning/test hook: pin the 16-bit GEMM tile configuration for all later launches in this
  * process (0, 1, 5, 11), or -1 to restore the automatic per-shape choice. */
 int f5h_gemm_force_config(int32_t cfg);
+/* Test hook (host only, no device needed): the batch path's pad-row skip test of a GEMM row tile
+ * (modules.py:551-553): 1 if rows [m0, m0 + BM) of an M-row operand hold a live row, where sequence s owns
+ * rows [s*live_seq, (s+1)*live_seq) and its first live_len[s] rows are live; 0 if every row is padding.
+ * The device kernels run the same function (kernels.h tile_live_rows). */
+int f5h_debug_tile_live(const int32_t* live_len, int32_t live_seq, int32_t M, int32_t m0, int32_t BM);
 
 /* ---------------------------------------------------------------------------------------
  * Vocos decoder (mel -> waveform), SURVEY §8(f1): the step after the CFM path, replacing

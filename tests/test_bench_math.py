@@ -148,6 +148,26 @@ def test_gpus_n_starts_n_ranks_and_prints_one_line():
     assert d["utterances_gathered"] == 8 and d["steps"] == 2
 
 
+def test_launcher_parent_makes_no_hip_call(monkeypatch, capsys):
+    """launch_ranks counts GPUs in a child process: with every torch entry that could reach the HIP runtime
+    made to raise in this (parent) process, `--gpus 8` on a box with fewer GPUs (none here) still exits 2 with
+    the message, and the parent's CUDA/HIP state stays uninitialised (bench.py:launch_ranks)."""
+    import torch
+
+    def boom(*a, **k):
+        raise AssertionError("the launcher parent touched the GPU runtime")
+
+    monkeypatch.setattr(torch.cuda, "device_count", boom)
+    monkeypatch.setattr(torch._C, "_cuda_getDeviceCount", boom)
+    monkeypatch.setattr(torch.cuda, "is_available", boom)
+    monkeypatch.setattr(torch.cuda, "init", boom)
+    args = bench.parse_args(["--gpus", "8", "--steps", "1", "--warmup", "0"])
+    rc = bench.launch_ranks(args, ["--gpus", "8", "--steps", "1", "--warmup", "0"])
+    assert rc == 2
+    assert "--gpus 8 but only" in capsys.readouterr().err
+    assert not torch.cuda.is_initialized()
+
+
 def test_outer_launcher_world_size_mismatch_fails():
     r = _bench_cmd("--gpus", "2", "--standin", "--steps", "1", "--warmup", "0",
                    env={"WORLD_SIZE": "3", "RANK": "0", "LOCAL_RANK": "0"})

@@ -147,6 +147,24 @@ def test_op_attention(compute, tol, S, H, N, masked):
 
 
 @pytest.mark.parametrize("compute", ["bf16", "fp16"])
+@pytest.mark.parametrize("N", [577, 65, 1876])
+def test_op_attention_ragged_tile_reads_no_foreign_rows(compute, N):
+    """N % 64 != 0: the last K/V tile's rows past N must read as zero, not as the next (sequence, head)'s keys
+    or the memory after V (the O buffer). The workspace is filled with NaN bits before the call:
+    any foreign row that reaches the P.V MFMA (0 * NaN) makes the output NaN."""
+    _need_gpu()
+    S, H = 2, 4
+    g = torch.Generator(device="cpu").manual_seed(N)
+    Q, K, V = (torch.randn(S, H, N, 64, generator=g).to(DEV) for _ in range(3))
+    O = op_attention(Q, K, V, None, compute=compute, poison=True)
+    assert torch.isfinite(O).all()
+    ref = torch.nn.functional.scaled_dot_product_attention(Q.double(), K.double(), V.double())
+    ref = ref.transpose(1, 2).reshape(S, N, H * 64)
+    err = (O.double() - ref).abs().max().item() / ref.abs().max().item()
+    assert err < (2e-2 if compute == "bf16" else 4e-3), err
+
+
+@pytest.mark.parametrize("compute", ["bf16", "fp16"])
 @pytest.mark.parametrize("spike", [0.0, 12.0, 160.0])
 def test_op_attention_rare_branches(compute, spike):
     """The 16-bit attention kernel against an fp64 softmax of the SAME rounded operands (the

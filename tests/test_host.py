@@ -97,3 +97,32 @@ def test_mel_front_end_requires_gpu_tensor():
     m = MelSpec()
     with pytest.raises(RuntimeError, match="GPU"):
         m(torch.randn(1, 24000))
+
+
+def _tile_live(live_len, live_seq, M, m0, BM):
+    import ctypes
+
+    from f5_tts_amd import _lib
+
+    arr = (ctypes.c_int32 * len(live_len))(*live_len)
+    return _lib.lib().f5h_debug_tile_live(ctypes.cast(arr, ctypes.c_void_p), live_seq, M, m0, BM)
+
+
+def test_pad_skip_tile_test_of_the_library():
+    """The GEMM kernels' pad-row skip test (kernels.h tile_live_rows, run on the host through the C ABI; no
+    device needed), against a brute-force row scan. Includes a short sequence after a long one: a tile that
+    starts in the long sequence's padding and ends inside the short one's padding holds no live row."""
+    cases = [([300, 20], 320), ([320, 1], 320), ([17, 300, 5, 320], 320), ([0, 64, 0], 100), ([5, 5, 5, 5], 64)]
+    for live_len, live_seq in cases:
+        M = live_seq * len(live_len)
+        live = np.zeros(M, bool)
+        for s, n in enumerate(live_len):
+            live[s * live_seq:s * live_seq + n] = True
+        for BM in (64, 128, 192, 256):
+            for m0 in range(0, M, BM):
+                want = bool(live[m0:m0 + BM].any())
+                assert _tile_live(live_len, live_seq, M, m0, BM) == int(want), (live_len, BM, m0)
+    # a tile spanning a sequence boundary with no live row on either side (the earlier test called it live)
+    assert _tile_live([300, 20], 320, 640, 384, 128) == 0
+    assert _tile_live([300, 0], 320, 640, 304, 256) == 0
+    assert _tile_live([300, 1], 320, 640, 304, 256) == 1
