@@ -6,11 +6,14 @@
 //     workgroup per CU at C2 (grid 8 x 32).
 //   * S^T = K . Q^T on v_mfma_f32_32x32x16_{bf16,f16}: the query sits on the lane (column), so a
 //     lane owns one query row's running max (row max = in-register max + one permlane32 swap).
-//   * lazy running max folded into the MFMA: after the first tile the S^T accumulator starts at
-//     -m_run, so the MFMA returns s - m_run; while no row's tile max exceeds m_run by more than
-//     THR (log2 units) p = exp2(s - m_run) needs no subtraction and O is never rescaled
-//     (P <= 2^THR). A wave that sees a larger jump re-bases: m_run += d, O, l *= 2^-d, s -= d
-//     (cdna_hip_programming.md T13; the branch is forced by the spike tests).
+//   * running max folded into the MFMA, set once: after the first tile the S^T accumulator starts at
+//     -m_run (m_run = the row's first-tile max), so the MFMA returns s - m_run and p = exp2(s - m_run)
+//     needs no subtraction. Later tiles take no row max at all (round 5): P may exceed 1, which the fp32
+//     O / l accumulators and the 16-bit P hold at full relative precision as long as P stays finite in the
+//     operand type; after the loop every row checks l <= 2^64 (bf16) / 2^15 (fp16), which bounds every P,
+//     and a workgroup with a failing row (a score more than that far above its first-tile max) reruns its
+//     key loop in the lazy-max form of cdna_hip_programming.md T13 (per-tile max, re-base past 2^8; forced
+//     by the spike tests and by f5h_attn_force_safe).
 //   * row sums on the VALU from the fp32 exp2s: 16 packed adds per tile and wave, issued in the
 //     MFMA shadow with the packs (the matrix-pipe form l^T += ones . P^T cost 4 of 20 MFMAs per tile).
 //   * the QK^T chains start from a loop-carried -m_run block (rewritten only on a re-base), and P
@@ -120,10 +123,14 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn16_kernel(AttnArgs a) {
     const int p = (r * NW + wid) * 64 + lane, row = p >> 3, slot = p & 7;
     dvoff[r] = (uint32_t)(row * 128 + swz128(row, slot) * 16);  // bytes: row, swizzled source chunk
   }
-  auto dma = [&](int buf, int kt) {
+  // live: kt < ntile (so kt*64 < L); otherwise the tile may lie wholly past L (the prologue's tiles 1 and 2)
+  auto dma = [&](int buf, int kt, bool live = false) {
     uint4* Ks = lds + buf * (TILE_B / 16);
     uint4* Vs = Ks + 512;
-    const uint32_t ext = (uint32_t)max(0, min(64, L - kt * 64)) * 128u;
+    // wave-uniform by construction; readfirstlane makes it provably so (else the descriptor sits in VGPRs and
+    // hipcc wraps every DMA piece in a waterfall loop, cdna_hip_programming.md T20)
+    const int rows = live ? min(64, L - kt * 64) : max(0, min(64, L - kt * 64));
+    const uint32_t ext = (uint32_t)__builtin_amdgcn_readfirstlane(rows * 128);
     const __amdgpu_buffer_rsrc_t krs = rsrc_of(K + (int64_t)kt * 4096, ext);
     const __amdgpu_buffer_rsrc_t vrs = rsrc_of(V + (int64_t)kt * 4096, ext);
 #pragma unroll
@@ -191,8 +198,22 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn16_kernel(AttnArgs a) {
       for (int j = 0; j < 8; ++j) qf[ks][j] = from_f32<T>(to_f32(qf[ks][j]) * c);
     }
   }
-  // the tile loop unrolled by the ring depth, so a tile's slot (and every LDS read offset) is a constant
-  auto tile = [&](auto SLOT, const int kt) {
+  // per-wave dead rows (batch path pad skip, q_len): a wave whose 32 query rows all lie past q_len keeps its
+  // share of the K/V DMA and the barriers (the ring is shared by the workgroup) but computes and stores
+  // nothing, so its SIMD partner issues alone (waves w and w + 4 share a SIMD; the dead rows are the last ones)
+  const bool wave_dead = a.q_len && (qb * (32 * NW) + wid_s * 32) >= a.q_len[s_idx];
+  constexpr float LMAX = std::is_same<T, f16>::value ? 32768.f : 0x1p64f;  // fp16 P must stay below 65504
+
+  // One K/V tile. FIRST (tile 0): the running max m_run starts at the tile's row max. Later tiles are
+  // exponentiated against m_run as it stands (no per-tile row max, no re-base test: 16 v_max3, a permlane
+  // and the vote per tile and wave are gone): P = 2^(s - m_run) may exceed 1, which the fp32 O and l
+  // accumulators and the 16-bit P carry exactly as well (relative precision does not depend on magnitude),
+  // as long as P stays finite in the operand type -- checked once per row after the loop (l <= LMAX bounds
+  // every P). SAFE (the rerun of a workgroup where a row failed that check, i.e. some score ran more than
+  // log2(LMAX) above its row's first-tile max): the lazy running max of cdna_hip_programming.md T13 -- per
+  // tile row max, re-base when it exceeds m_run by more than THR.
+  auto tile = [&](auto SLOT, auto FIRST_, auto SAFE_, const int kt) {
+    constexpr bool FIRST = decltype(FIRST_)::value, SAFE = decltype(SAFE_)::value;
     // tile kt landed for this wave's own DMA (tile kt+1 may stay in flight); the barrier
     // publishes every wave's part of it and retires all reads of slot (kt+3)%4 (= tile kt-1).
     if (kt + 2 < ntile)
@@ -202,7 +223,7 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn16_kernel(AttnArgs a) {
     else
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
-    if (kt == 0) probe_mark(a.probe, probe_t, 1);
+    if (FIRST && !SAFE) probe_mark(a.probe, probe_t, 1);
     constexpr int slot = decltype(SLOT)::value;
     constexpr uint32_t so = (uint32_t)(slot * TILE_B);  // ring slot offset: an immediate of every LDS read
 
@@ -212,7 +233,7 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn16_kernel(AttnArgs a) {
       kf[0][ks] = lds_b128<so>(kaddr[ks]);
       kf[1][ks] = lds_b128<so + 4096>(kaddr[ks]);
     });
-    if (kt + 3 < ntile) dma((slot + 3) % NS, kt + 3);
+    if (kt + 3 < ntile) dma((slot + 3) % NS, kt + 3, true);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 #pragma unroll
     for (int t = 0; t < 2; ++t)
@@ -232,8 +253,7 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn16_kernel(AttnArgs a) {
       });
     };
 
-    // ---- S^T - m_run = K Q^T + (-m_run): both chains start from minit, which is rewritten only
-    // when m_run changes (no per-tile accumulator initialisation)
+    // ---- S^T - m_run = K Q^T + (-m_run): both chains start from minit (= -m_run in every slot; zero in tile 0)
     f32x16 sacc[2];
 #pragma unroll
     for (int t = 0; t < 2; ++t) {
@@ -241,8 +261,7 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn16_kernel(AttnArgs a) {
 #pragma unroll
       for (int ks = 1; ks < 4; ++ks) sacc[t] = OP::mma32(__builtin_bit_cast(v8, kf[t][ks]), qf[ks], sacc[t]);
     }
-    // both halves of V^T now: their LDS latency hides under the row max and the first exp2 chunk (read
-    // after the max, hipcc hoisted the exp2s above them and the wait before the first PV MFMA exposed it)
+    // both halves of V^T now: their LDS latency hides under the exp2 of the first chunk
     vread(std::integral_constant<int, 0>{});
     vread(std::integral_constant<int, 1>{});
     if (kt * 64 + 64 > klen) {  // ragged last tile: keys past klen get p = 0
@@ -253,37 +272,39 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn16_kernel(AttnArgs a) {
         for (int r = 0; r < 16; ++r)
           if (kbase + t * 32 + (r & 3) + 8 * (r >> 2) >= klen) sacc[t][r] = -INFINITY;
     }
-    float mx = -INFINITY;
-#pragma unroll
-    for (int t = 0; t < 2; ++t)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) mx = fmaxf(mx, sacc[t][r]);
-    mx = fmaxf(mx, xor32(mx));
-    if (kt == 0) {
-      // first tile (>= 1 valid key): the running max starts at the tile max
-      m_run = mx;
+    if constexpr (FIRST || SAFE) {
+      float mx = -INFINITY;
 #pragma unroll
       for (int t = 0; t < 2; ++t)
 #pragma unroll
-        for (int r = 0; r < 16; ++r) sacc[t][r] -= mx;
+        for (int r = 0; r < 16; ++r) mx = fmaxf(mx, sacc[t][r]);
+      mx = fmaxf(mx, xor32(mx));
+      if constexpr (FIRST) {
+        // first tile (>= 1 valid key): the running max starts at the tile max
+        m_run = mx;
 #pragma unroll
-      for (int r = 0; r < 16; ++r) minit[r] = -m_run;
-    } else if (!__all(mx <= THR)) {
-      // re-base the rows whose scores ran more than THR above m_run (rare: early tiles)
-      const float d = fmaxf(mx, 0.f);
-      const float alpha = __builtin_amdgcn_exp2f(-d);
-      m_run += d;
+        for (int t = 0; t < 2; ++t)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        oacc[0][r] *= alpha;
-        oacc[1][r] *= alpha;
-        minit[r] = -m_run;
+          for (int r = 0; r < 16; ++r) sacc[t][r] -= mx;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) minit[r] = -m_run;
+      } else if (!__all(mx <= THR)) {
+        // re-base the rows whose scores ran more than THR above m_run (rare: early tiles)
+        const float d = fmaxf(mx, 0.f);
+        const float alpha = __builtin_amdgcn_exp2f(-d);
+        m_run += d;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          oacc[0][r] *= alpha;
+          oacc[1][r] *= alpha;
+          minit[r] = -m_run;
+        }
+#pragma unroll
+        for (int t = 0; t < 2; ++t)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) sacc[t][r] -= d;
+        lrow *= alpha;
       }
-#pragma unroll
-      for (int t = 0; t < 2; ++t)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) sacc[t][r] -= d;
-      lrow *= alpha;
     }
     // exp2 / pack of 16-key chunk c = (t, sx) of P (row sums from the fp32 exp2s, four packed
     // adds), then its two MFMAs (both O^T halves), issued between chunk c+1's exp2s and packs: a
@@ -334,21 +355,74 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn16_kernel(AttnArgs a) {
     });
     mma_chunk(std::integral_constant<int, 3>{});
   };
-  for (int kt0 = 0; kt0 < ntile; kt0 += NS) {
-    static_for<0, NS>([&](auto S) {
-      const int kt = kt0 + decltype(S)::value;
-      if (kt < ntile) tile(S, kt);
-    });
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no LDS-DMA outlives the loop (ntile == 0 included)
-  probe_mark(a.probe, probe_t, 2);
+  using IF = std::false_type;
+  using IT = std::true_type;
+  // all tiles: tile 0 peeled (FIRST), the rest unrolled by the ring depth so every slot is a constant
+  // A dead wave runs the same waits, barriers and DMA share in a loop of its own (a branch inside the tile
+  // would make hipcc copy the O accumulators back at every tile's join)
+  auto pass = [&](auto SAFE_) {
+    if (wave_dead) {
+      for (int kt = 0; kt < ntile; ++kt) {
+        if (kt + 2 < ntile)
+          asm volatile("s_waitcnt vmcnt(%0)" ::"i"(4 * CPW) : "memory");
+        else if (kt + 1 < ntile)
+          asm volatile("s_waitcnt vmcnt(%0)" ::"i"(2 * CPW) : "memory");
+        else
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        if (kt + 3 < ntile) dma((kt + 3) % NS, kt + 3, true);
+      }
+    } else {
+      if (ntile > 0) tile(std::integral_constant<int, 0>{}, IT{}, SAFE_, 0);
+      for (int kt0 = 0; kt0 < ntile; kt0 += NS) {
+        static_for<0, NS>([&](auto S) {
+          const int kt = kt0 + decltype(S)::value;
+          if (kt >= 1 && kt < ntile) tile(S, IF{}, SAFE_, kt);
+        });
+      }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no LDS-DMA outlives the loop (ntile == 0 included)
+  };
+  pass(IF{});
   float l_tot = lrow.x + lrow.y;
   l_tot += xor32(l_tot);  // lanes l and l + 32 hold the two key halves of one query
+  {
+    // Did any row of the workgroup exceed LMAX (or overflow)? One word per wave in the ring's first bytes
+    // (all reads of the last tile retired: every wave waited for its LDS reads before its last MFMAs).
+    const bool bad = !(l_tot <= LMAX);
+    const unsigned vote = __builtin_amdgcn_ballot_w64(bad) != 0ull ? 1u : 0u;
+    __builtin_amdgcn_s_barrier();
+    uint32_t* flags = reinterpret_cast<uint32_t*>(lds);
+    if (lane == 0) flags[wid] = vote;
+    __syncthreads();
+    unsigned any = 0;
+#pragma unroll
+    for (int w = 0; w < NW; ++w) any |= flags[w];
+    if (__builtin_amdgcn_readfirstlane(any) || a.force_safe) {
+      // rare: rerun the whole key loop with the lazy running max (SAFE)
+      __syncthreads();  // every wave has read the flags before the DMA overwrites them
+      m_run = 0.f;
+      lrow = f2{0.f, 0.f};
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        oacc[0][r] = 0.f;
+        oacc[1][r] = 0.f;
+        minit[r] = 0.f;
+      }
+      dma(0, 0);
+      dma(1, 1);
+      dma(2, 2);
+      pass(IT{});
+      l_tot = lrow.x + lrow.y;
+      l_tot += xor32(l_tot);
+    }
+  }
+  probe_mark(a.probe, probe_t, 2);
   const float inv = l_tot > 0.f ? 1.f / l_tot : 0.f;
   // Epilogue (T21): lane l < 32 holds columns 8k..8k+3 of its row, lane l + 32 columns 8k+4..8k+7; one
   // permlane32 swap per dword pairs groups k and k+1, so every lane stores 16 contiguous bytes
   // (lower lanes group k, upper lanes group k+1): 4 dwordx4 stores instead of 8 dwordx2
-  {
+  if (!wave_dead) {
     T* O = reinterpret_cast<T*>(a.o) + (((int64_t)s_idx * L + min(qrow, L - 1)) * a.H + head) * 64;
 #pragma unroll
     for (int u = 0; u < 2; ++u)
@@ -445,8 +519,13 @@ static void launch16(const AttnArgs& a, hipStream_t st) {
     hipLaunchKernelGGL((attn16_kernel<T, false, NW>), grid, dim3(64 * NW), 0, st, a);
 }
 
-hipError_t attention(int compute, const AttnArgs& a, hipStream_t st) {
-  if (a.S <= 0 || a.H <= 0 || a.L <= 0) return hipErrorInvalidValue;
+static int g_force_safe = 0;
+void attention_force_safe(int on) { g_force_safe = on ? 1 : 0; }
+
+hipError_t attention(int compute, const AttnArgs& a0, hipStream_t st) {
+  if (a0.S <= 0 || a0.H <= 0 || a0.L <= 0) return hipErrorInvalidValue;
+  AttnArgs a = a0;
+  a.force_safe = g_force_safe;
   switch (compute) {
     case F5H_C_BF16: launch16<bf16>(a, st); break;
     case F5H_C_FP16: launch16<f16>(a, st); break;

@@ -1570,6 +1570,12 @@ int f5h_gemm_force_config(int32_t cfg) {
   return 0;
 }
 
+int f5h_attn_force_safe(int32_t on) {
+  attention_force_safe(on);
+  g_kernel_epoch.fetch_add(1);  // captured graphs hold the old kernel arguments
+  return 0;
+}
+
 int f5h_debug_tile_live(const int32_t* live_len, int32_t live_seq, int32_t M, int32_t m0, int32_t BM) {
   if (live_seq <= 0 || M <= 0 || BM <= 0 || m0 < 0 || m0 >= M) return fail(F5H_EINVAL, "bad tile");
   return tile_live_rows(live_len, live_seq, M, m0, BM) ? 1 : 0;

@@ -99,8 +99,11 @@ struct AttnArgs {
   float scale;            // 1/sqrt(64)
   int prescaled;          // q already carries scale*log2(e): scores are in log2 units
   DevProbe probe;         // in-kernel launch timing (null slots: off)
+  int force_safe;         // test hook: every workgroup reruns its key loop in the lazy-max form (attention.hip)
 };
 hipError_t attention(int compute, const AttnArgs& a, hipStream_t st);
+// test hook (f5h_attn_force_safe): 1 = every later 16-bit attention launch takes the SAFE rerun
+void attention_force_safe(int on);
 
 // grouped conv1d k=31, 16 groups, pad 15 (ConvPositionEmbedding, modules.py:175-201)
 struct ConvArgs {

@@ -42,6 +42,7 @@ EXPORTS = (
     "f5h_op_linear",
     "f5h_op_attention",
     "f5h_gemm_force_config",
+    "f5h_attn_force_safe",
     "f5h_debug_tile_live",
     "f5h_vocos_create",
     "f5h_vocos_destroy",
@@ -156,6 +157,8 @@ def lib():
     L.f5h_op_attention.restype = ctypes.c_int
     L.f5h_gemm_force_config.argtypes = [i32]
     L.f5h_gemm_force_config.restype = ctypes.c_int
+    L.f5h_attn_force_safe.argtypes = [i32]
+    L.f5h_attn_force_safe.restype = ctypes.c_int
     L.f5h_debug_tile_live.argtypes = [vp, i32, i32, i32, i32]
     L.f5h_debug_tile_live.restype = ctypes.c_int
     L.f5h_vocos_create.argtypes = [ctypes.POINTER(VocosArch), ctypes.POINTER(Weight), i32, i32, ctypes.POINTER(vp)]

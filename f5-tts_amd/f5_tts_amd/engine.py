@@ -274,6 +274,11 @@ def op_attention(Q, K, V, kv_len=None, compute="bf16", q_prescaled=False, poison
     return O
 
 
+def attn_force_safe(on: bool):
+    """Test hook: every later 16-bit attention launch reruns its key loop in the lazy-running-max form."""
+    _lib.check(_lib.lib().f5h_attn_force_safe(int(bool(on))), "attn_force_safe")
+
+
 def gemm_force_config(cfg: int = -1):
     """Pin the 16-bit GEMM tile configuration (0, 1, 5, 11) for this process; -1 = automatic."""
     _lib.check(_lib.lib().f5h_gemm_force_config(int(cfg)), "gemm_force_config")

@@ -228,6 +228,10 @@ int f5h_op_attention(void* stream, int32_t compute, int32_t S, int32_t H, int32_
 /* Tuning/test hook: pin the 16-bit GEMM tile configuration for all later launches in this
  * process (0, 1, 5, 11), or -1 to restore the automatic per-shape choice. */
 int f5h_gemm_force_config(int32_t cfg);
+/* Test hook: on != 0 makes every later 16-bit attention launch of this process rerun each workgroup's key
+ * loop in its lazy-running-max form (the path a row takes when a score runs far above its first tile's max;
+ * attention.hip), 0 restores the default. Results agree to rounding (tests/test_gpu_parity.py). */
+int f5h_attn_force_safe(int32_t on);
 /* Test hook (host only, no device needed): the batch path's pad-row skip test of a GEMM row tile
  * (modules.py:551-553): 1 if rows [m0, m0 + BM) of an M-row operand hold a live row, where sequence s owns
  * rows [s*live_seq, (s+1)*live_seq) and its first live_len[s] rows are live; 0 if every row is padding.

@@ -165,14 +165,27 @@ def test_op_attention_ragged_tile_reads_no_foreign_rows(compute, N):
 
 
 @pytest.mark.parametrize("compute", ["bf16", "fp16"])
-@pytest.mark.parametrize("spike", [0.0, 12.0, 160.0])
-def test_op_attention_rare_branches(compute, spike):
+@pytest.mark.parametrize("spike", [0.0, 12.0, 20.0, 70.0, 160.0])
+@pytest.mark.parametrize("safe", [False, True])
+def test_op_attention_rare_branches(compute, spike, safe):
     """The 16-bit attention kernel against an fp64 softmax of the SAME rounded operands (the
     engine's layout: q pre-multiplied by (1/8)*log2(e), scores in log2 units), with inputs that
     force the rare branches (cdna_hip_programming.md rule 26): one key row at a late tile is
-    aligned with a few query rows so their scores jump far above the first tile's. spike 12:
-    past the lazy-rescale threshold (2^8); spike 160: ~160 log2 units (re-base far beyond it)."""
+    aligned with a few query rows so their scores jump far above the first tile's. Against the first
+    tile's max, P reaches ~2^spike: spike 12 stays in the fast path in both dtypes (P carried above 1),
+    20 passes fp16's bound (2^15: the workgroup reruns in the lazy-max form), 70 bf16's (2^64), 160 both.
+    safe=True forces that rerun everywhere (the lazy-max form alone, incl. its re-base past 2^8)."""
     _need_gpu()
+    from f5_tts_amd.engine import attn_force_safe
+
+    attn_force_safe(safe)
+    try:
+        _rare_branch_case(compute, spike)
+    finally:
+        attn_force_safe(False)
+
+
+def _rare_branch_case(compute, spike):
     S, H, N = 2, 2, 700
     g = torch.Generator(device="cpu").manual_seed(11)
     Q, K, V = (torch.randn(S, H, N, 64, generator=g) for _ in range(3))

@@ -1,37 +1,57 @@
-"""Vendor-library yardstick for the path's shapes (not on the product path): hipBLASLt GEMMs via
-torch.mm (bf16) and torch SDPA (bf16) at C2/C3 shapes. Run under rocprofv3 --kernel-trace --stats
-and read per-kernel averages; prints wall-clock per op as well."""
+"""Vendor-library yardstick for the path's shapes (not on the product path): hipBLASLt GEMMs via torch.mm
+(bf16, no epilogue) and torch SDPA (bf16, head dim 64, non-causal) at the C2 (S = 2) and C4-per-rank / C3
+(S = 64, padded to 1876 frames) shapes of every kernel class. Run under `rocprofv3 --kernel-trace --stats` to
+get the per-kernel averages; also prints / writes event-timed averages per op (20 back-to-back launches).
+
+  python tools/vendor_ref.py [out.json]
+"""
+import json
+import sys
+
 import torch
 import torch.nn.functional as F
 
 dev = "cuda:0"
-SH = {"c2_qkv": (3752, 3072, 1024), "c2_ffn1": (3752, 2048, 1024), "c2_out": (3752, 1024, 1024),
-      "c2_ffn2": (3752, 1024, 2048), "c3_qkv": (120064, 3072, 1024), "c3_ffn2": (120064, 1024, 2048)}
+N_FR, D, F_DIM = 1876, 1024, 2048
+SH = {}
+for cfg, S in (("c2", 2), ("c4", 64)):
+    M = S * N_FR
+    SH[f"{cfg}_qkv"] = (M, 3 * D, D)
+    SH[f"{cfg}_out"] = (M, D, D)
+    SH[f"{cfg}_ffn1"] = (M, F_DIM, D)
+    SH[f"{cfg}_ffn2"] = (M, D, F_DIM)
+
+
+def timed(fn, reps):
+    for _ in range(3):
+        fn()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        fn()
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / reps * 1e3  # us
+
+
+res = {"device": torch.cuda.get_device_name(0), "torch": torch.__version__, "ops": {}}
+g = torch.Generator(device=dev).manual_seed(0)
 for name, (M, N, K) in SH.items():
-    A = torch.randn(M, K, device=dev, dtype=torch.bfloat16)
-    W = torch.randn(N, K, device=dev, dtype=torch.bfloat16)
-    for _ in range(3):
-        C = A @ W.t()
-    torch.cuda.synchronize()
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    e0.record()
-    R = 20
-    for _ in range(R):
-        C = A @ W.t()
-    e1.record()
-    torch.cuda.synchronize()
-    ms = e0.elapsed_time(e1) / R
-    print(f"{name}: {ms*1e3:.1f} us  {2*M*N*K/ms/1e9:.0f} TF/s", flush=True)
-for S, H, N in ((2, 16, 1876), (64, 16, 1876)):
-    q, k, v = (torch.randn(S, H, N, 64, device=dev, dtype=torch.bfloat16) for _ in range(3))
-    for _ in range(3):
-        o = F.scaled_dot_product_attention(q, k, v)
-    torch.cuda.synchronize()
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    e0.record()
-    for _ in range(10):
-        o = F.scaled_dot_product_attention(q, k, v)
-    e1.record()
-    torch.cuda.synchronize()
-    ms = e0.elapsed_time(e1) / 10
-    print(f"sdpa S={S}: {ms*1e3:.1f} us  {4*S*H*N*N*64/ms/1e9:.0f} TF/s", flush=True)
+    A = torch.randn(M, K, device=dev, dtype=torch.bfloat16, generator=g)
+    W = torch.randn(N, K, device=dev, dtype=torch.bfloat16, generator=g)
+    us = timed(lambda: A @ W.t(), 20 if M < 10000 else 5)
+    tf = 2 * M * N * K / us / 1e6
+    res["ops"][name] = {"kind": "hipBLASLt torch.mm bf16", "M": M, "N": N, "K": K, "us": us, "tflops": tf,
+                        "frac": tf / 2500.0}
+    print(f"{name}: {us:.1f} us  {tf:.0f} TF/s", flush=True)
+    del A, W
+for cfg, S in (("c2", 2), ("c4", 64)):
+    q, k, v = (torch.randn(S, 16, N_FR, 64, device=dev, dtype=torch.bfloat16, generator=g) for _ in range(3))
+    us = timed(lambda: F.scaled_dot_product_attention(q, k, v), 10 if S < 10 else 3)
+    tf = 4 * S * 16 * N_FR * N_FR * 64 / us / 1e6
+    res["ops"][f"{cfg}_attention"] = {"kind": "torch SDPA bf16", "S": S, "H": 16, "N": N_FR, "us": us,
+                                      "tflops": tf, "frac": tf / 2500.0}
+    print(f"sdpa {cfg} S={S}: {us:.1f} us  {tf:.0f} TF/s", flush=True)
+if len(sys.argv) > 1:
+    json.dump(res, open(sys.argv[1], "w"), indent=1)
