@@ -73,19 +73,53 @@ def _same_shape(a, b, match_compute=True):
     return a.get("config") is None or b.get("config") is None or a["config"] == b["config"]
 
 
+PROFILES = os.path.join(REPO, "profiles")  # committed summaries (older rounds' files live in profiles/archive/)
+_SRC_HASH = None
+
+
+def src_hash():
+    """Content hash of the engine's sources (f5-tts_amd/csrc, include/f5h.h): what a profile summary was
+    measured with (summaries record it as "src_hash", with the git "head" they were committed from), so a
+    bench line can say whether an attached summary matches the library it ran."""
+    global _SRC_HASH
+    if _SRC_HASH is None:
+        import glob
+        import hashlib
+
+        h = hashlib.sha256()
+        files = sorted(glob.glob(os.path.join(REPO, "f5-tts_amd", "csrc", "*")))
+        files.append(os.path.join(REPO, "include", "f5h.h"))
+        for f in files:
+            if os.path.isfile(f) and (f.endswith((".hip", ".h", ".cpp")) or os.path.basename(f) == "Makefile"):
+                h.update(os.path.basename(f).encode())
+                h.update(open(f, "rb").read())
+        _SRC_HASH = h.hexdigest()[:16]
+    return _SRC_HASH
+
+
+def summary_stamp():
+    """The provenance fields a profile summary carries (tools/class_profile.py, tools/pmc_classes.py):
+    the git head it was measured at (F5H_HEAD, passed in by the launching script: the GPU box has no .git)
+    and the source hash of the tree it ran."""
+    return {"head": os.environ.get("F5H_HEAD", "unknown"), "src_hash": src_hash()}
+
+
 def profile_class(pattern, kernel_class, shape, match_compute=True):
     """A kernel class's entry in the newest committed profile summary (profiles/<pattern>, written by
-    tools/pmc_classes.py or tools/class_profile.py) measured at this launch shape, and its source file.
-    Summaries of other shapes are never attached (None, reason)."""
+    tools/pmc_classes.py or tools/class_profile.py) measured at this launch shape, its source file, and its
+    provenance {"head", "src_hash", "matches_build"}: the git head the summary was measured at and whether its
+    source hash is this tree's. Summaries of other shapes are never attached (None, reason, None)."""
     import glob
-    files = sorted(glob.glob(os.path.join(REPO, "profiles", pattern)))
+    files = sorted(glob.glob(os.path.join(PROFILES, pattern)))
     if not files:
-        return None, None
+        return None, None, None
     for f in reversed(files):
         d = json.load(open(f))
         if _same_shape(d.get("shape"), shape, match_compute):
-            return d.get("classes", {}).get(kernel_class), os.path.relpath(f, REPO)
-    return None, f"no profiles/{pattern} summary at shape {shape} (newest: {os.path.relpath(files[-1], REPO)})"
+            prov = {"head": d.get("head"), "src_hash": d.get("src_hash"),
+                    "matches_build": d.get("src_hash") == src_hash()}
+            return d.get("classes", {}).get(kernel_class), os.path.relpath(f, REPO), prov
+    return None, f"no profiles/{pattern} summary at shape {shape} (newest: {os.path.relpath(files[-1], REPO)})", None
 
 
 def pmc_traffic(kernel_class, shape):
@@ -93,8 +127,8 @@ def pmc_traffic(kernel_class, shape):
     launch shape (profiles/*_pmc_classes.json, tools/pmc_classes.py: separate FETCH_SIZE and WRITE_SIZE
     passes, 2 x FETCH_SIZE (gfx950 counts half of wide streaming reads, MI355X_MICROARCH.md §HBM) +
     WRITE_SIZE), and its source file; other shapes get None. Bytes do not depend on the 16-bit type."""
-    ent, src = profile_class("*_pmc_classes*.json", kernel_class, shape, match_compute=False)
-    return (ent["hbm_bytes"] if ent else None), src
+    ent, src, prov = profile_class("*_pmc_classes*.json", kernel_class, shape, match_compute=False)
+    return (ent["hbm_bytes"] if ent else None), src, prov
 
 
 def build_model(preset, compute, device):
@@ -296,24 +330,28 @@ def class_entry(kc, avg_ms, n, arch, S, L, launches_per_call, ms_call, chains=1,
         e.update(bound="hbm", achieved=round(ach, 1), peak=PEAK_HBM_GBPS, unit="GB/s",
                  frac=round(ach / PEAK_HBM_GBPS, 4), bytes_per_launch=by)
     shape = {"S": S, "L": L, "dim": arch["dim"], "depth": arch["depth"], "config": config, "compute": compute}
-    traffic, src = pmc_traffic(kc, shape)
+    traffic, src, tprov = pmc_traffic(kc, shape)
     e["traffic"] = traffic
     e["traffic_source"] = src
+    if tprov:
+        e["traffic_provenance"] = tprov
     # the same class in the committed rocprofv3 kernel trace (profiler timestamps, dispatch ramp included)
-    rp, rsrc = profile_class("*_rocprof_classes*.json", kc, shape)
+    rp, rsrc, rprov = profile_class("*_rocprof_classes*.json", kc, shape)
     if rp:
         e["rocprof_avg_launch_us"] = rp["avg_launch_us"]
         e["rocprof_source"] = rsrc
+        e["rocprof_provenance"] = rprov
         if fl:
             e["rocprof_frac"] = round(fl / (rp["avg_launch_us"] * 1e-6) / 1e12 / PEAK_BF16_TFLOPS, 4)
         elif e.get("bytes_per_launch"):
             e["rocprof_frac"] = round(e["bytes_per_launch"] / (rp["avg_launch_us"] * 1e-6) / 1e9 / PEAK_HBM_GBPS, 4)
     # MFMA utilisation and stall split from the committed SQ counter passes (tools/class_profile.py pmc)
-    mf, msrc = profile_class("*_pmc_mfma*.json", kc, shape)
+    mf, msrc, mprov = profile_class("*_pmc_mfma*.json", kc, shape)
     if mf:
         e["pmc"] = {k: mf[k] for k in ("mfma_busy", "wait_frac", "issue_stall_frac", "active_frac",
                                        "coexec_over_mfma", "valu_per_mfma", "clock_ghz") if k in mf}
         e["pmc_source"] = msrc
+        e["pmc_provenance"] = mprov
     if traffic and kc in ("qkv", "out", "ffn1", "ffn2", "attention", "conv"):
         d, ff = arch["dim"], int(arch["dim"] * arch["ff_mult"])
         kn = {"qkv": (d, 3 * d), "out": (d, d), "ffn1": (d, ff), "ffn2": (ff, d)}.get(kc)

@@ -50,25 +50,65 @@ def test_norm_bytes_follow_the_residual_width():
     assert bench.class_bytes("norm", unett, S, L, esz=4) == S * L * 1024 * (4 + 4)
 
 
-def test_pmc_traffic_only_at_the_measured_shape():
+def _summary(path, shape, classes, head="abc1234", src="match"):
+    import json
+
+    d = {"shape": shape, "classes": classes, "head": head,
+         "src_hash": bench.src_hash() if src == "match" else src}
+    path.write_text(json.dumps(d))
+
+
+@pytest.fixture
+def fake_profiles(tmp_path, monkeypatch):
+    """A profiles/ directory of stamped summaries (the committed ones change every round; these pin the
+    attachment rules): PMC traffic at C2/C3/C4/C5, a C2 kernel trace and C2 SQ counters (bf16)."""
+    c2 = {"S": 2, "L": 1876, "dim": 1024, "depth": 22}
+    _summary(tmp_path / "r05_pmc_classes_c2.json", c2,
+             {"attention": {"hbm_bytes": 30.9e6}, "qkv": {"hbm_bytes": 84.1e6},
+              "conv": {"hbm_bytes": 2 * 1876 * 1024 * 7 + 1024 * 64 * 31 * 2}})
+    _summary(tmp_path / "r05_pmc_classes_c3.json", dict(c2, S=64, config="c3"), {"qkv": {"hbm_bytes": 2.3e9}})
+    _summary(tmp_path / "r05_pmc_classes_c4.json", dict(c2, S=64, config="c4"), {"qkv": {"hbm_bytes": 2.2e9}},
+             src="0000000000000000")
+    _summary(tmp_path / "r05_pmc_classes_c5.json", {"S": 16, "L": 1877, "dim": 1024, "depth": 24, "config": "c5"},
+             {"ffn1": {"hbm_bytes": 1.1e9}})
+    _summary(tmp_path / "r05_rocprof_classes_c2.json", dict(c2, config="c2"), {"attention": {"avg_launch_us": 35.0}})
+    _summary(tmp_path / "r05_pmc_mfma_c2.json", dict(c2, config="c2"), {"attention": {"mfma_busy": 0.4}})
+    monkeypatch.setattr(bench, "PROFILES", str(tmp_path))
+    return tmp_path
+
+
+def test_pmc_traffic_only_at_the_measured_shape(fake_profiles):
     """A committed PMC summary is attached to a bench line only at the launch shape it was measured on
     (C2: S=2, N=1876, Base; C3/C4: S=64 and the workload named; C5: S=16, N=1877, UNetT depth 24); any
-    other shape or workload reports no traffic."""
+    other shape or workload reports no traffic. Every attached summary names the git head it was measured
+    at and whether its engine source hash is this tree's."""
     c2 = {"S": 2, "L": 1876, "dim": 1024, "depth": 22}
-    t, src = bench.pmc_traffic("attention", c2)
-    assert t and t > 0 and src.startswith("profiles/")
-    t, src = bench.pmc_traffic("attention", dict(c2, S=8))
-    assert t is None and "no profiles" in src
-    t3, src3 = bench.pmc_traffic("qkv", dict(c2, S=64, config="c3"))
-    t4, src4 = bench.pmc_traffic("qkv", dict(c2, S=64, config="c4"))
+    t, src, prov = bench.pmc_traffic("attention", c2)
+    assert t and t > 0 and "r05_pmc_classes_c2" in src
+    assert prov == {"head": "abc1234", "src_hash": bench.src_hash(), "matches_build": True}
+    t, src, prov = bench.pmc_traffic("attention", dict(c2, S=8))
+    assert t is None and "no profiles" in src and prov is None
+    t3, src3, p3 = bench.pmc_traffic("qkv", dict(c2, S=64, config="c3"))
+    t4, src4, p4 = bench.pmc_traffic("qkv", dict(c2, S=64, config="c4"))
     assert "c3" in src3 and "c4" in src4 and t3 != t4
-    t, src = bench.pmc_traffic("qkv", dict(c2, S=64, config="c9"))
+    assert p3["matches_build"] and not p4["matches_build"]  # the C4 summary came from other sources
+    t, src, _ = bench.pmc_traffic("qkv", dict(c2, S=64, config="c9"))
     assert t is None and "no profiles" in src
-    t, src = bench.pmc_traffic("ffn1", {"S": 16, "L": 1877, "dim": 1024, "depth": 24, "config": "c5"})
+    t, src, _ = bench.pmc_traffic("ffn1", {"S": 16, "L": 1877, "dim": 1024, "depth": 24, "config": "c5"})
     assert t and "c5" in src
 
 
-def test_timing_summaries_only_for_the_measured_compute_type():
+def test_attached_summaries_name_their_source_commit(fake_profiles):
+    """A bench line's class entry carries, beside every attached summary (traffic, kernel trace, SQ counters),
+    the commit the summary was measured at and whether it matches the library's sources."""
+    arch = configs.get_arch("F5TTS_v1_Base")
+    e = bench.class_entry("attention", 0.036, 8, arch, 2, 1876, 352, 52.0, 1, config="c2", compute="bf16")
+    for k in ("traffic", "rocprof", "pmc"):
+        prov = e[k + "_provenance"]
+        assert prov["head"] == "abc1234" and prov["matches_build"] is True, k
+
+
+def test_timing_summaries_only_for_the_measured_compute_type(fake_profiles):
     """The committed kernel-trace averages and SQ counters (measured in bf16) are attached to a bf16 line
     only: an fp16 line at the same shape gets neither (fp16 runs the same cycles at a lower clock), while
     the byte traffic, which does not depend on the 16-bit type, is attached to both."""
@@ -80,18 +120,17 @@ def test_timing_summaries_only_for_the_measured_compute_type():
     assert bf["traffic"] and fp["traffic"] == bf["traffic"]
 
 
-def test_conv_class_traffic_over_algorithmic():
+def test_conv_class_traffic_over_algorithmic(fake_profiles):
     """The conv position embedding class carries its PMC traffic and algorithmic bytes (the mean of its two
     grouped conv layers: fp32 input + 16-bit output, then 16-bit input + fp32 residual + 16-bit output; plus
-    the 16 groups' 31-tap weights) at the C2 shape. Since the group-major XCD map (round 4) the measured
-    traffic is ~1.0x that (3.2x before: every XCD re-fetched every group's tap panel)."""
+    the 16 groups' 31-tap weights) at the C2 shape."""
     arch = configs.get_arch("F5TTS_v1_Base")
     e = bench.class_entry("conv", 0.0257, 8, arch, 2, 1876, 16, 50.9, 1)
     assert e["algorithmic_bytes"] == 2 * 1876 * 1024 * 7 + 1024 * 64 * 31 * 2
     assert e["traffic"] and 0.8 < e["traffic_over_algorithmic"] < 1.5
 
 
-# avg launch (us) per class measured by the round-3 final benches (profiles/r03_final_bench_c{2,4,5}.log),
+# avg launch (us) per class measured by the round-3 final benches (profiles/archive/r03_final_bench_c{2,4,5}.log),
 # the shapes they ran at, and the compute width: every class's fraction of its roofline must be <= 1
 _R03 = {
     ("F5TTS_v1_Base", 2, 1876): {"qkv": 26.459, "attention": 39.594, "out": 13.812, "norm": 6.341, "ffn1": 21.227,
@@ -203,14 +242,18 @@ def test_pad_skip_prices_attention_and_out_on_live_rows():
     assert same["flops_per_launch"] == bench.class_flops("attention", arch, S, L)
 
 
-def test_live_row_traffic_pricing_at_c3():
+def test_live_row_traffic_pricing_at_c3(fake_profiles):
     """With the pad-row skip (ragged C3 batch) attention reads K and V of every row but Q and O of the live
-    query rows only, and the out-projection touches live rows only: their algorithmic bytes count those rows,
-    so the measured traffic of the committed C3 PMC summary is >= ~1x of them (it was 0.86x / 0.95x of the
-    padded count)."""
+    query rows only, and the out-projection touches live rows only: their algorithmic bytes count those rows
+    (round 4's C3 PMC summary measured 1.0-1.2x of them; 0.86x / 0.95x of the padded count)."""
     arch = configs.get_arch("F5TTS_v1_Base")
     tot = [564 + (i * 1312) // 31 for i in range(32)]
     q = tot * 2  # CFG copies
+    c3 = {"S": 64, "L": 1876, "dim": 1024, "depth": 22, "config": "c3"}
+    live_attn = 2 * 2 * 16 * 64 * (64 * 1876 + sum(q))
+    live_out = 2 * (sum(q) * 1024 + 1024 * 1024) + 2 * 2 * sum(q) * 1024
+    _summary(fake_profiles / "r05_pmc_classes_c3.json", c3,
+             {"attention": {"hbm_bytes": 1.01 * live_attn}, "out": {"hbm_bytes": 1.2 * live_out}})
     at = bench.class_entry("attention", 1.058, 8, arch, 64, 1876, 704, 2262.0, 1, config="c3", qlens=q)
     assert at["algorithmic_bytes"] == 2 * 2 * 16 * 64 * (64 * 1876 + sum(q))
     out = bench.class_entry("out", 0.300, 8, arch, 64, 1876, 704, 2262.0, 1, config="c3", qlens=q)

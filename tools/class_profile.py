@@ -39,6 +39,17 @@ SHAPES = {c: {k: s[k] for k in ("config", "S", "L", "dim", "depth")} for c, s in
 NSIMD = 1024  # 256 CUs x 4 SIMDs
 
 
+
+def _stamp():
+    """Provenance of a summary (bench.summary_stamp): the git head (F5H_HEAD) and the engine source hash."""
+    import os
+    import sys
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    if repo not in sys.path:
+        sys.path.insert(0, repo)
+    import bench
+    return bench.summary_stamp()
+
 def _trace_rows(path):
     rows = sorted(csv.DictReader(open(path)), key=lambda r: int(r["Dispatch_Id"]))
     return [(int(r["Dispatch_Id"]), r["Kernel_Name"], (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
@@ -56,7 +67,7 @@ def trace(path, config, out):
                "dispatches": len(v)} for c, v in acc.items()}
     j = {"note": f"rocprofv3 --kernel-trace of tools/trace_c2.py run {config} (warm + marked CFM.sample calls); "
                  f"per class mean/median dispatch duration (End - Start), classes by position around attention",
-         "source": path, "shape": SHAPES[config], "classes": res}
+         "source": path, "shape": SHAPES[config], "classes": res, **_stamp()}
     json.dump(j, open(out, "w"), indent=1)
     print(json.dumps(j, indent=1))
 
@@ -133,7 +144,7 @@ def pmc(config, out, *paths):
                  f"tools/trace_c2.py run {config} in the shipped graph mode; median per dispatch of each class; "
                  f"SQ_WAVE_CYCLES/WAIT_*/ACTIVE_* in quad-cycles, MFMA_BUSY in cycles; derived metrics in "
                  f"tools/class_profile.py",
-         "sources": list(paths), "shape": SHAPES[config], "grbm_fit": fit, "classes": res}
+         "sources": list(paths), "shape": SHAPES[config], "grbm_fit": fit, "classes": res, **_stamp()}
     json.dump(j, open(out, "w"), indent=1)
     print(json.dumps(j, indent=1))
 

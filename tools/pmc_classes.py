@@ -31,6 +31,17 @@ SHAPES = {"c2": dict(config="c2", S=2, L=1876, dim=1024, depth=22, ff=2048),
           "c5": dict(config="c5", S=16, L=1877, dim=1024, depth=24, ff=4096)}  # UNetT: + the time token
 
 
+
+def _stamp():
+    """Provenance of a summary (bench.summary_stamp): the git head (F5H_HEAD) and the engine source hash."""
+    import os
+    import sys
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    if repo not in sys.path:
+        sys.path.insert(0, repo)
+    import bench
+    return bench.summary_stamp()
+
 def load(path, counter):
     rows = {}
     for r in csv.DictReader(open(path)):
@@ -104,6 +115,7 @@ def main(fpath, wpath, out, config="c2"):
          # committed before it had none)
          "shape": {k: shp[k] for k in ("S", "L", "dim", "depth")} | ({"config": config} if config != "c2" else {}),
          "classes": res}
+    j.update(_stamp())
     json.dump(j, open(out, "w"), indent=1)
     print(json.dumps(j, indent=1))
 
