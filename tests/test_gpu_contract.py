@@ -429,11 +429,19 @@ def test_engine_drop_never_waits_for_other_streams():
     t0 = time.perf_counter()
     pygc.collect()
     gc_alone = time.perf_counter() - t0  # the collector's own cost on this heap
-    other, third = torch.cuda.Stream(), torch.cuda.Stream()
+    # `other` carries the spin. `third` is a high-priority stream: HIP gives each stream priority its own
+    # hardware queues, so its kernel cannot queue behind the spin (round 4: with both at the default
+    # priority, a third-stream op waited 0.78 s behind the spin -- streams share hardware queues under
+    # GPU_MAX_HW_QUEUES = 4 -- while the releases themselves returned in microseconds). `same` is a second
+    # default-priority stream, reported for the record only (it may or may not share the spin's queue).
+    other = torch.cuda.Stream()
+    third = torch.cuda.Stream(priority=-1)
+    same = torch.cuda.Stream()
     x = torch.randn(4096, device=DEV)
-    with torch.cuda.stream(third):  # the third-stream op once beforehand: its first launch loads the kernel
-        _ = x * 2.0
-    third.synchronize()
+    for s_ in (third, same):  # each stream's op once beforehand: the first launch loads the kernel
+        with torch.cuda.stream(s_):
+            _ = x * 2.0
+        s_.synchronize()
     with torch.cuda.stream(other):
         torch.cuda._sleep(int(2.0e9))  # ~1 s of spinning on another stream
     t_spin = time.perf_counter()
@@ -461,26 +469,35 @@ def test_engine_drop_never_waits_for_other_streams():
     finally:
         for n in names:
             setattr(L, n, orig[n])
-    # another stream's launch is not held up on the host (a hipFree in the release would block every HIP call
-    # of the process until the spin ends). Only the enqueue is timed: with GPU_MAX_HW_QUEUES streams share
-    # hardware queues, so the kernel itself may queue behind the spin; its result is checked afterwards.
+    # another stream's work is neither held up on the host (a hipFree in the release would block every HIP
+    # call of the process until the spin ends) nor on the device: the high-priority stream's kernel COMPLETES
+    # while the spin still runs
     t0 = time.perf_counter()
     with torch.cuda.stream(third):
         y = x * 2.0
+    third.synchronize()
     third_op = time.perf_counter() - t0
+    t0 = time.perf_counter()
+    with torch.cuda.stream(same):
+        z = x * 3.0
+    same_enqueue = time.perf_counter() - t0
     t0 = time.perf_counter()
     still_busy = not other.query()
     query = time.perf_counter() - t0
     elapsed = time.perf_counter() - t_spin
-    print(f"drop {took:.4f}s (gc alone {gc_alone:.4f}s), releases {calls}, third-stream op {third_op:.4f}s, "
-          f"query {query:.4f}s, {elapsed:.3f}s after the spin started")
+    same.synchronize()
+    same_done = time.perf_counter() - t_spin
+    print(f"drop {took:.4f}s (gc alone {gc_alone:.4f}s), releases {calls}; high-priority stream (priority "
+          f"{third.priority}) op completed in {third_op:.4f}s; default-priority stream (priority {same.priority}) "
+          f"op enqueued in {same_enqueue:.4f}s, completed {same_done:.3f}s after the spin started; query "
+          f"{query:.4f}s, {elapsed:.3f}s after the spin started")
     assert still_busy, f"the spin kernel ended {elapsed:.3f}s in, before the checks: raise its length"
     assert set(calls) == set(names), calls
     assert max(max(v) for v in calls.values()) < 0.05, calls  # each release returns at once
     assert took < 0.5, took  # the whole drop (collector included) does not wait for the 1 s spin
-    assert third_op < 0.05 and query < 0.05, (third_op, query)
-    third.synchronize()
-    assert torch.equal(y, x * 2.0)
+    assert third_op < 0.05, third_op  # completed, not only enqueued, during the spin
+    assert same_enqueue < 0.05 and query < 0.05, (same_enqueue, query)
+    assert torch.equal(y, x * 2.0) and torch.equal(z, x * 3.0)
     _lib.lib().f5h_release_pending(1)  # returns once the releases ran (after the spin, on the reaper)
     assert _lib.lib().f5h_release_pending(0) == 0
     m2 = _model(gc.arch_of("tiny"), "bf16")
