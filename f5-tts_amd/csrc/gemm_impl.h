@@ -303,43 +303,47 @@ F5H_DEV void store8_rs(__amdgpu_buffer_rsrc_t r, uint32_t elem, const V8& x) {
   }
 }
 
-// Fast epilogue of one wave's sub-tile (whole-column tiles of the hot epilogues), per 16-row strip:
-// accumulators -> the wave's LDS strip (fp32, EPAD-float rows) -> 8-column chunks of whole rows. A lane's
-// column chunk is the same in every strip, so bias/gate/QKV head indices are loaded once, and the row
-// data of strip i+1 (RoPE pairs, residual rows, row-mask bytes) is fetched before strip i stores.
-// The strip loop has no control flow: bias presence is a template choice, per-lane choices (RoPE on
-// this column, rows past M) are selects or the store descriptor's range check. Any branch or any
-// arithmetic on a just-loaded value makes hipcc wait for that load, and on gfx9 every store issued
-// before it counts in the same vmcnt: at C3 such waits made the 256x256 ping-pong epilogue 13-15 us per
-// tile (profiles/r03_timeline_c3.txt). rbase/cbase: the sub-tile's first row/column.
-// Shared by gemm_kernel and gemm_pp_kernel.
-template <typename TC, int EPI, int MT, int NT, int WN, int EPAD, bool PREF, bool BIAS, int PM, int PT>
-F5H_DEV void epilogue_fast_t(const GemmArgs& g, const f32x4 (&acc)[MT][NT], float* Cs, int rbase, int cbase,
-                             int lane, const V8 (&pre)[PM][PT]) {
-  constexpr int CH = WN / 8;          // 8-column chunks per strip row
-  constexpr int TPC = 16 * CH / 64;   // chunks per lane per strip
-  static_assert(64 % CH == 0 && (16 * CH) % 64 == 0, "whole chunks per lane");
+// Direct epilogue (round 5): the MFMAs run with swapped operands (W fragment as A, activation fragment as B),
+// so accumulator acc[i][j] holds C^T: lane l has row 16i + (l & 15) and the FOUR CONSECUTIVE columns
+// 16j + 4(l >> 4) + r (r = 0..3). One v_permlane16_swap per dword between blocks j and j+1 (the odd 16-lane
+// rows of block j trade with the even rows of block j+1) leaves every lane with EIGHT consecutive columns of
+// its row: lanes of row q = l >> 4 hold block j + (q & 1), columns 8 (q >> 1) .. +7 (cdna_hip_programming.md
+// T21, with the 16-lane swap). The epilogue then works on registers only: no accumulator round trip through
+// LDS (the fast epilogue before it wrote every fp32 accumulator to an LDS strip with 4-byte stores and read it
+// back by rows: 256 KB per 256x256 tile, ~1.6 us of LDS write bandwidth alone), no per-strip wave barriers.
+// Per element the arithmetic is the same functions as before (bitwise identical results). The row data of
+// strip i+1 (RoPE pairs, residual chunks, row-mask bytes, addends) is fetched before strip i stores.
+// pre: PREF residual chunks prefetched before the K loop, [MT][NT/2].
+template <typename TC, int EPI, int MT, int NT, bool PREF, bool BIAS, int PM, int PT>
+F5H_DEV void epilogue_direct_t(const GemmArgs& g, const f32x4 (&acc)[MT][NT], int rbase, int cbase, int lane,
+                               const V8 (&pre)[PM][PT]) {
+  static_assert(NT % 2 == 0, "column blocks in pairs");
+  constexpr int NP = NT / 2;
   const int fr = lane & 15, q = lane >> 4;
-  const int cc = lane % CH;
-  const int col = cbase + cc * 8;
-  V8 bias8 = V8{};
-  if constexpr (BIAS) bias8 = load8(g.bias + col);
-  V8 gate8 = V8{{1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f}};
-  if constexpr (EPI == EPI_RESID || EPI == EPI_RESID16)
-    if (g.gate) gate8 = load8(g.gate + col);
-  int which = 0, head = 0, dh = 0;
+  const int coff = 16 * (q & 1) + 8 * (q >> 1);  // the lane's 8-column chunk within a pair of 16-column blocks
+  V8 bias8[NP], gate8[NP];
+  int colp[NP];
+#pragma unroll
+  for (int jp = 0; jp < NP; ++jp) {
+    colp[jp] = cbase + 32 * jp + coff;
+    bias8[jp] = V8{};
+    if constexpr (BIAS) bias8[jp] = load8(g.bias + colp[jp]);
+    gate8[jp] = V8{{1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f}};
+    if constexpr (EPI == EPI_RESID || EPI == EPI_RESID16)
+      if (g.gate) gate8[jp] = load8(g.gate + colp[jp]);
+  }
+  int which = 0, head = 0, dh[NP];
   bool rope_on = false;
   float qsc = 1.f;
   __amdgpu_buffer_rsrc_t dst;
   if constexpr (EPI == EPI_QKV) {
-    // a wave's 64 columns are one head of one of q/k/v (cbase % 64 == 0): wave-uniform, so the
-    // destination descriptor lives in scalar registers (a per-lane one costs a waterfall loop per store)
-    static_assert(WN <= 64 && 64 % WN == 0, "a wave's columns lie in one head");
+    // a wave's columns lie in one head of one of q/k/v (cbase % 32 == 0, <= 64 columns from a head start):
+    // wave-uniform, so the destination descriptor lives in scalar registers
     const int inner = g.heads * 64;
     which = __builtin_amdgcn_readfirstlane(fdiv(cbase, inner));
-    const int hc = col - which * inner;
-    head = hc >> 6;
-    dh = hc & 63;
+    head = __builtin_amdgcn_readfirstlane((cbase - which * inner) >> 6);
+#pragma unroll
+    for (int jp = 0; jp < NP; ++jp) dh[jp] = (colp[jp] - which * inner) & 63;
     rope_on = which < 2 && head < g.rope_heads;
     qsc = (which == 0 && g.q_scale != 0.f) ? g.q_scale : 1.f;
     dst = rsrc_of(which == 0 ? g.q : (which == 1 ? g.k : g.v), (uint64_t)g.M * inner * sizeof(TC));
@@ -347,26 +351,22 @@ F5H_DEV void epilogue_fast_t(const GemmArgs& g, const f32x4 (&acc)[MT][NT], floa
     constexpr int OES = (EPI == EPI_STORE || EPI == EPI_RESID || EPI == EPI_INPROJ) ? 4 : (int)sizeof(TC);
     dst = rsrc_of(g.C, (uint64_t)(g.M + (EPI == EPI_INPROJ ? g.dual_rows : 0)) * g.ldc * OES);
   }
-  // Loads only, raw bits, no arithmetic on their results here (see above): conversions happen at the
-  // use, one strip later. Row indices are clamped instead of branched on (rows >= M are never stored).
+  // Loads only, raw bits, no arithmetic on their results here: conversions happen at the use, one strip
+  // later (a branch or arithmetic on a just-loaded value makes hipcc wait for it, behind every older store).
+  // Row indices are clamped instead of branched on (rows >= M are never stored).
   struct RowIn {
-    u32x4 d0, d1;  // RoPE (cos, sin) of four pairs (QKV, fp32), the residual row chunk (RESID), the addend (INPROJ)
+    u32x4 d0, d1;  // RoPE (cos, sin) of four pairs (QKV), the residual chunk (RESID), the addend (INPROJ)
     u32x4 e0, e1;  // INPROJ: the second output row's addend
-    uint32_t kb;   // RESID row-mask byte
   };
   const __amdgpu_buffer_rsrc_t rk = rsrc_of(g.rowkeep, g.rowkeep ? (uint64_t)g.M : 0);  // null: reads 0
   const bool masked = g.rowkeep != nullptr;
-  // QKV: (sequence, position) of each of the lane's chunk rows, for the strip being fetched (pf) and the one being
-  // stored (ps), advanced by 16 rows per strip (one division per chunk row for the whole epilogue, not two per
-  // strip). Rows past M get positions too: the RoPE table index stays in range and their stores are dropped.
-  int pf_sq[TPC], pf_pos[TPC], ps_sq[TPC], ps_pos[TPC];
+  // QKV: (sequence, position) of the lane's row for the strip being fetched (pf) and the one being stored (ps),
+  // advanced by 16 rows per strip. Rows past M get positions too: the RoPE index stays in range, stores drop.
+  int pf_sq = 0, pf_pos = 0, ps_sq = 0, ps_pos = 0;
   if constexpr (EPI == EPI_QKV) {
-#pragma unroll
-    for (int t = 0; t < TPC; ++t) {
-      const int row0 = rbase + t * (64 / CH) + lane / CH;
-      pf_sq[t] = ps_sq[t] = fdiv(row0, g.seq_len);
-      pf_pos[t] = ps_pos[t] = row0 - pf_sq[t] * g.seq_len;
-    }
+    const int row0 = rbase + fr;
+    pf_sq = ps_sq = fdiv(row0, g.seq_len);
+    pf_pos = ps_pos = row0 - pf_sq * g.seq_len;
   }
   auto advance = [&](int& sq, int& pos) {
     pos += 16;
@@ -375,34 +375,33 @@ F5H_DEV void epilogue_fast_t(const GemmArgs& g, const f32x4 (&acc)[MT][NT], floa
       ++sq;
     }
   };
-  auto fetch = [&](int i, RowIn (&ri)[TPC]) {
+  uint32_t kb[2] = {0u, 0u};
+  auto fetch = [&](int i, RowIn (&ri)[NP], uint32_t& kbi) {
+    const int rowc = min(rbase + i * 16 + fr, g.M - 1);
 #pragma unroll
-    for (int t = 0; t < TPC; ++t) {
-      const int rr = t * (64 / CH) + lane / CH;
-      const int rowc = min(rbase + i * 16 + rr, g.M - 1);
+    for (int jp = 0; jp < NP; ++jp) {
       if constexpr (EPI == EPI_QKV) {
-        (void)rowc;
-        const u32x4* p = reinterpret_cast<const u32x4*>(g.rope + pf_pos[t] * 32 + (dh >> 1));
-        ri[t].d0 = p[0];
-        ri[t].d1 = p[1];
-        advance(pf_sq[t], pf_pos[t]);
+        const u32x4* p = reinterpret_cast<const u32x4*>(g.rope + pf_pos * 32 + (dh[jp] >> 1));
+        ri[jp].d0 = p[0];
+        ri[jp].d1 = p[1];
       } else if constexpr (EPI == EPI_RESID || EPI == EPI_RESID16) {
         if constexpr (!PREF) {
           const u32x4* p = reinterpret_cast<const u32x4*>(reinterpret_cast<const ResT<TC, EPI>*>(
-                                                              g.resid ? g.resid : g.C) + (int64_t)rowc * g.ldc + col);
-          ri[t].d0 = p[0];
-          if constexpr (sizeof(ResT<TC, EPI>) == 4) ri[t].d1 = p[1];  // fp32 rows: 32 B
+                                                              g.resid ? g.resid : g.C) + (int64_t)rowc * g.ldc + colp[jp]);
+          ri[jp].d0 = p[0];
+          if constexpr (sizeof(ResT<TC, EPI>) == 4) ri[jp].d1 = p[1];  // fp32 rows: 32 B
         }
-        ri[t].kb = __builtin_amdgcn_raw_buffer_load_b8(rk, (uint32_t)rowc, 0, 0);
       } else if constexpr (EPI == EPI_INPROJ) {
-        const u32x4* p = reinterpret_cast<const u32x4*>(g.add + (int64_t)rowc * g.ld_add + col);
-        ri[t].d0 = p[0];
-        ri[t].d1 = p[1];
-        const u32x4* p2 = reinterpret_cast<const u32x4*>(g.add + (int64_t)(rowc + g.dual_rows) * g.ld_add + col);
-        ri[t].e0 = p2[0];  // (rows [M, M + dual_rows) of the addend; the first rows again when dual_rows = 0)
-        ri[t].e1 = p2[1];
+        const u32x4* p = reinterpret_cast<const u32x4*>(g.add + (int64_t)rowc * g.ld_add + colp[jp]);
+        ri[jp].d0 = p[0];
+        ri[jp].d1 = p[1];
+        const u32x4* p2 = reinterpret_cast<const u32x4*>(g.add + (int64_t)(rowc + g.dual_rows) * g.ld_add + colp[jp]);
+        ri[jp].e0 = p2[0];  // (rows [M, M + dual_rows) of the addend; the first rows again when dual_rows = 0)
+        ri[jp].e1 = p2[1];
       }
     }
+    if constexpr (EPI == EPI_QKV) advance(pf_sq, pf_pos);
+    if constexpr (EPI == EPI_RESID || EPI == EPI_RESID16) kbi = __builtin_amdgcn_raw_buffer_load_b8(rk, (uint32_t)rowc, 0, 0);
   };
   // the raw row data as 8 fp32 values
   auto as_v8 = [&](const RowIn& ri) -> V8 {
@@ -417,30 +416,29 @@ F5H_DEV void epilogue_fast_t(const GemmArgs& g, const f32x4 (&acc)[MT][NT], floa
                  __uint_as_float(ri.d1[2]), __uint_as_float(ri.d1[3])}};
     }
   };
-  RowIn rbuf[2][TPC];
-  fetch(0, rbuf[0]);
+  RowIn rbuf[2][NP];
+  fetch(0, rbuf[0], kb[0]);
   static_for<0, MT>([&](auto I) {
     constexpr int i = decltype(I)::value;
-    if constexpr (i + 1 < MT) fetch(i + 1, rbuf[(i + 1) & 1]);
+    if constexpr (i + 1 < MT) fetch(i + 1, rbuf[(i + 1) & 1], kb[(i + 1) & 1]);
+    const int row = rbase + i * 16 + fr;  // rows >= M: dropped by the store descriptor
 #pragma unroll
-    for (int j = 0; j < NT; ++j)
+    for (int jp = 0; jp < NP; ++jp) {
+      // blocks 2jp and 2jp+1 -> this lane's 8 consecutive columns colp[jp] .. +7
+      V8 x;
 #pragma unroll
-      for (int r = 0; r < 4; ++r) Cs[(q * 4 + r) * EPAD + j * 16 + fr] = acc[i][j][r];
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-#pragma unroll
-    for (int t = 0; t < TPC; ++t) {
-      const int rr = t * (64 / CH) + lane / CH;
-      const int row = rbase + i * 16 + rr;  // rows >= M: dropped by the store descriptor
-      const float* src = Cs + rr * EPAD + cc * 8;
-      const float4 a0 = *reinterpret_cast<const float4*>(src), a1 = *reinterpret_cast<const float4*>(src + 4);
-      V8 x{{a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w}};
+      for (int r = 0; r < 4; ++r) {
+        const auto sw = __builtin_amdgcn_permlane16_swap(__float_as_uint(acc[i][2 * jp][r]),
+                                                         __float_as_uint(acc[i][2 * jp + 1][r]), false, false);
+        x.v[r] = __uint_as_float(sw[0]);
+        x.v[r + 4] = __uint_as_float(sw[1]);
+      }
+      const int col = colp[jp];
       if constexpr (BIAS) {
 #pragma unroll
-        for (int e = 0; e < 8; ++e) x.v[e] = add_nc(x.v[e], bias8.v[e]);
+        for (int e = 0; e < 8; ++e) x.v[e] = add_nc(x.v[e], bias8[jp].v[e]);
       }
-      const RowIn& ri = rbuf[i & 1][t];
+      const RowIn& ri = rbuf[i & 1][jp];
       if constexpr (EPI == EPI_QKV) {
         const V8 cs = as_v8(ri);
         // interleaved pairs (a, b) -> (a c - b s, b c + a s) as packed products and one packed add (each
@@ -449,29 +447,28 @@ F5H_DEV void epilogue_fast_t(const GemmArgs& g, const f32x4 (&acc)[MT][NT], floa
         for (int p = 0; p < 4; ++p) {
           const float c = cs.v[2 * p], sn = cs.v[2 * p + 1];
           const f32x2 ab = {x.v[2 * p], x.v[2 * p + 1]};
-          f32x2 r;
+          f32x2 rr;
           {
 #pragma clang fp contract(off)
             const f32x2 pc = ab * c, ps = f32x2{ab.y, ab.x} * sn;
-            r = pc + f32x2{-ps.x, ps.y};
-            r = (rope_on ? r : ab) * qsc;  // exact for qsc = 1 (k, v columns)
+            rr = pc + f32x2{-ps.x, ps.y};
+            rr = (rope_on ? rr : ab) * qsc;  // exact for qsc = 1 (k, v columns)
           }
-          x.v[2 * p] = r.x;
-          x.v[2 * p + 1] = r.y;
+          x.v[2 * p] = rr.x;
+          x.v[2 * p + 1] = rr.y;
         }
         (void)row;
-        store8_rs<TC>(dst, (uint32_t)(((ps_sq[t] * g.heads + head) * g.seq_len + ps_pos[t]) * 64 + dh), x);
-        advance(ps_sq[t], ps_pos[t]);
+        store8_rs<TC>(dst, (uint32_t)(((ps_sq * g.heads + head) * g.seq_len + ps_pos) * 64 + dh[jp]), x);
       } else if constexpr (EPI == EPI_RESID || EPI == EPI_RESID16) {
         V8 c;
         if constexpr (PREF)
-          c = pre[PREF ? i : 0][PREF ? t : 0];
+          c = pre[PREF ? i : 0][PREF ? jp : 0];
         else
           c = as_v8(ri);
-        const bool keep = !masked || ri.kb;
+        const bool keep = !masked || kb[i & 1];
         V8 o;
 #pragma unroll
-        for (int e = 0; e < 8; ++e) o.v[e] = resid_add(c.v[e], gate8.v[e], x.v[e], keep);
+        for (int e = 0; e < 8; ++e) o.v[e] = resid_add(c.v[e], gate8[jp].v[e], x.v[e], keep);
         store8_rs<ResT<TC, EPI>>(dst, (uint32_t)((int64_t)row * g.ldc + col), o);
       } else if constexpr (EPI == EPI_GELU_TANH || EPI == EPI_GELU_ERF_OP) {
         if constexpr (EPI == EPI_GELU_TANH && is16<TC>()) {
@@ -508,19 +505,18 @@ F5H_DEV void epilogue_fast_t(const GemmArgs& g, const f32x4 (&acc)[MT][NT], floa
         store8_rs<float>(dst, (uint32_t)((int64_t)row * g.ldc + col), x);
       }
     }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    if constexpr (EPI == EPI_QKV) advance(ps_sq, ps_pos);
   });
 }
-template <typename TC, int EPI, int MT, int NT, int WN, int EPAD, bool PREF, int PM, int PT>
-F5H_DEV void epilogue_fast(const GemmArgs& g, const f32x4 (&acc)[MT][NT], float* Cs, int rbase, int cbase,
-                           int lane, const V8 (&pre)[PM][PT]) {
+template <typename TC, int EPI, int MT, int NT, bool PREF, int PM, int PT>
+F5H_DEV void epilogue_direct(const GemmArgs& g, const f32x4 (&acc)[MT][NT], int rbase, int cbase, int lane,
+                             const V8 (&pre)[PM][PT]) {
   if (g.bias)
-    epilogue_fast_t<TC, EPI, MT, NT, WN, EPAD, PREF, true>(g, acc, Cs, rbase, cbase, lane, pre);
+    epilogue_direct_t<TC, EPI, MT, NT, PREF, true>(g, acc, rbase, cbase, lane, pre);
   else
-    epilogue_fast_t<TC, EPI, MT, NT, WN, EPAD, PREF, false>(g, acc, Cs, rbase, cbase, lane, pre);
+    epilogue_direct_t<TC, EPI, MT, NT, PREF, false>(g, acc, rbase, cbase, lane, pre);
 }
+
 
 // FAST: the launcher guarantees whole-column tiles (N % BN == 0, ldc % 8 == 0) for the hot
 // epilogues, so the epilogue is compiled without per-element column guards (see below).
@@ -635,29 +631,29 @@ __global__ __launch_bounds__(64 * WGM * WGN, 2) void gemm_kernel(GemmArgs g) {
   // operand stages (so they do not delay stage 0: the first wait leaves them in flight, the second
   // retires them), and the epilogue's read-modify-write does not expose a dependent HBM/MALL round
   // trip. Register budget: small tiles only.
-  constexpr int CH_ = WN / 8, TPS = 16 * CH_ / 64;
-  constexpr bool PREF = (EPI == EPI_RESID || EPI == EPI_RESID16) && is16<TC>() && (16 * CH_) % 64 == 0 &&
-                        MT * TPS * 8 <= 32;
-  V8 pre[PREF ? MT : 1][PREF ? TPS : 1];
+  // (the direct epilogue's layout: lane row 16i + (lane & 15), its 8-column chunk coff within each pair of
+  // 16-column blocks)
+  constexpr int NPAIR = NT / 2;
+  constexpr bool PREF = (EPI == EPI_RESID || EPI == EPI_RESID16) && is16<TC>() && NT % 2 == 0 &&
+                        MT * NPAIR * 8 <= 32;
+  V8 pre[PREF ? MT : 1][PREF ? NPAIR : 1];
   if constexpr (PREF) {
     const ResT<TC, EPI>* Cp = reinterpret_cast<const ResT<TC, EPI>*>(g.resid ? g.resid : g.C);
     const int fr_ = lane & 15, q_ = lane >> 4;
-    (void)fr_;
-    (void)q_;
+    const int coff = 16 * (q_ & 1) + 8 * (q_ >> 1);
 #pragma unroll
     for (int i = 0; i < MT; ++i)
 #pragma unroll
-      for (int t = 0; t < TPS; ++t) {
-        const int idx = t * 64 + lane, rr = idx / CH_, cc = idx % CH_;
-        const int row = m0 + wm * WM + i * 16 + rr, col = n0 + wn * WN + cc * 8;
+      for (int t = 0; t < NPAIR; ++t) {
+        const int row = m0 + wm * WM + i * 16 + fr_, col = n0 + wn * WN + 32 * t + coff;
         const bool ok = row < g.M && col + 8 <= g.N && g.ldc % 4 == 0;
-        // unconditional (a select on the address, no branch): the four loads issue back to back
+        // unconditional (a select on the address, no branch): the loads issue back to back
         // (a branch per load made hipcc wait for each one in turn); unused when !ok
         pre[i][t] = load8(Cp + (ok ? (int64_t)row * g.ldc + col : 0));
       }
   }
 
-  constexpr int NPRE = PREF ? MT * TPS : 0;  // residual loads issued behind the first stages
+  constexpr int NPRE = PREF ? MT * NPAIR : 0;  // residual loads issued behind the first stages
   for (int kt = 0; kt < nk; ++kt) {
     // stage kt has landed for THIS wave once at most the younger in-flight stages remain;
     // the barrier then publishes every wave's part of it
@@ -694,7 +690,7 @@ __global__ __launch_bounds__(64 * WGM * WGN, 2) void gemm_kernel(GemmArgs g) {
       for (int i = 0; i < MT; ++i)
 #pragma unroll
         for (int j = 0; j < NT; ++j)
-          acc[i][j] = Slab<TC>::mma(__builtin_bit_cast(frag, ar[0][i]), __builtin_bit_cast(frag, br[0][j]), acc[i][j]);
+          acc[i][j] = Slab<TC>::mma(__builtin_bit_cast(frag, br[0][j]), __builtin_bit_cast(frag, ar[0][i]), acc[i][j]);
       continue;
     } else {
     // slab 0's reads are the oldest MT+NT LDS ops: consume them while slab 1's land
@@ -708,7 +704,7 @@ __global__ __launch_bounds__(64 * WGM * WGN, 2) void gemm_kernel(GemmArgs g) {
     for (int i = 0; i < MT; ++i)
 #pragma unroll
       for (int j = 0; j < NT; ++j)
-        acc[i][j] = Slab<TC>::mma(__builtin_bit_cast(frag, ar[0][i]), __builtin_bit_cast(frag, br[0][j]), acc[i][j]);
+        acc[i][j] = Slab<TC>::mma(__builtin_bit_cast(frag, br[0][j]), __builtin_bit_cast(frag, ar[0][i]), acc[i][j]);
     __builtin_amdgcn_sched_barrier(0);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 #pragma unroll
@@ -720,7 +716,7 @@ __global__ __launch_bounds__(64 * WGM * WGN, 2) void gemm_kernel(GemmArgs g) {
     for (int i = 0; i < MT; ++i)
 #pragma unroll
       for (int j = 0; j < NT; ++j)
-        acc[i][j] = Slab<TC>::mma(__builtin_bit_cast(frag, ar[SLABS - 1][i]), __builtin_bit_cast(frag, br[SLABS - 1][j]),
+        acc[i][j] = Slab<TC>::mma(__builtin_bit_cast(frag, br[SLABS - 1][j]), __builtin_bit_cast(frag, ar[SLABS - 1][i]),
                                   acc[i][j]);
     }
   }
@@ -742,17 +738,16 @@ __global__ __launch_bounds__(64 * WGM * WGN, 2) void gemm_kernel(GemmArgs g) {
   // (RoPE pairs, residual rows, row masks) is fetched before strip i stores: no vmcnt wait in
   // the strip loop covers an older store (one strip of global round trips instead of one per
   // chunk; measured 9.5 us of a 30.6 us QKV launch before).
-  constexpr bool FAST_EPI = FAST && (64 % CH == 0) && (16 * CH) % 64 == 0;
+  constexpr bool FAST_EPI = FAST && NT % 2 == 0;
   if constexpr (FAST_EPI) {
-    epilogue_fast<TC, EPI, MT, NT, WN, C::EPAD, PREF>(g, acc, Cs, m0 + wm * WM, n0 + wn * WN, lane, pre);
+    epilogue_direct<TC, EPI, MT, NT, PREF>(g, acc, m0 + wm * WM, n0 + wn * WN, lane, pre);
   }
   if constexpr (!FAST_EPI) {
 #pragma unroll
     for (int i = 0; i < MT; ++i) {
+      // swapped-operand layout: the lane's row fr, four consecutive columns 16j + 4q
 #pragma unroll
-      for (int j = 0; j < NT; ++j)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) Cs[(q * 4 + r) * C::EPAD + j * 16 + fr] = acc[i][j][r];
+      for (int j = 0; j < NT; ++j) *reinterpret_cast<f32x4*>(Cs + fr * C::EPAD + j * 16 + 4 * q) = acc[i][j];
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -950,7 +945,7 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(GemmArgs g) {
       for (int i = 0; i < MT; ++i)
 #pragma unroll
         for (int j = 0; j < NT; ++j)
-          acc[i][j] = Op16<TC>::mma16(__builtin_bit_cast(v8, af[s][i]), __builtin_bit_cast(v8, bfr[s][j]), acc[i][j]);
+          acc[i][j] = Op16<TC>::mma16(__builtin_bit_cast(v8, bfr[s][j]), __builtin_bit_cast(v8, af[s][i]), acc[i][j]);
     __builtin_amdgcn_sched_barrier(0);
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
@@ -967,14 +962,13 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(GemmArgs g) {
     // whole-column tiles: the strip-pipelined epilogue (the generic one below waits out every strip's
     // residual / RoPE loads before its stores: 13-15 us per 256x256 tile at C3, profiles/r03_timeline_c3.txt)
     const V8 none[1][1] = {};
-    epilogue_fast<TC, EPI, MT, NT, WN, C::EPAD, false>(g, acc, Cs, rbase, cbase, lane, none);
+    epilogue_direct<TC, EPI, MT, NT, false>(g, acc, rbase, cbase, lane, none);
   } else {
 #pragma unroll
   for (int i = 0; i < MT; ++i) {
 #pragma unroll
     for (int j = 0; j < NT; ++j)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) Cs[(q * 4 + r) * C::EPAD + j * 16 + fr] = acc[i][j][r];
+      *reinterpret_cast<f32x4*>(Cs + fr * C::EPAD + j * 16 + 4 * q) = acc[i][j];  // swapped layout
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -1144,7 +1138,7 @@ __global__ __launch_bounds__(512, 1) void gemm_8p_kernel(GemmArgs g) {
       for (int j = 0; j < 2; ++j)
 #pragma unroll
         for (int s = 0; s < 2; ++s)
-          acc[ha][hb][i][j] = Op16<TC>::mma16(__builtin_bit_cast(v8, af[i][s]), __builtin_bit_cast(v8, bf[j][s]),
+          acc[ha][hb][i][j] = Op16<TC>::mma16(__builtin_bit_cast(v8, bf[j][s]), __builtin_bit_cast(v8, af[i][s]),
                                               acc[ha][hb][i][j]);
     __builtin_amdgcn_s_setprio(0);
     __builtin_amdgcn_sched_barrier(0);
@@ -1206,15 +1200,14 @@ __global__ __launch_bounds__(512, 1) void gemm_8p_kernel(GemmArgs g) {
     const int rbase = m0 + ha * 128 + wr * 64, cbase = n0 + hb * 128 + wc * QW;
     if constexpr (FAST) {
       const V8 none[1][1] = {};
-      epilogue_fast<TC, EPI, 4, 2, QW, EPAD, false>(g, acc[ha][hb], Cs, rbase, cbase, lane, none);
+      epilogue_direct<TC, EPI, 4, 2, false>(g, acc[ha][hb], rbase, cbase, lane, none);
     } else {
       constexpr int CH = QW / 8;
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
 #pragma unroll
         for (int j = 0; j < 2; ++j)
-#pragma unroll
-          for (int r = 0; r < 4; ++r) Cs[(q * 4 + r) * EPAD + j * 16 + fr] = acc[ha][hb][i][j][r];
+          *reinterpret_cast<f32x4*>(Cs + fr * EPAD + j * 16 + 4 * q) = acc[ha][hb][i][j];  // swapped layout
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");

@@ -157,10 +157,13 @@ def lib():
     L.f5h_op_attention.restype = ctypes.c_int
     L.f5h_gemm_force_config.argtypes = [i32]
     L.f5h_gemm_force_config.restype = ctypes.c_int
-    L.f5h_attn_force_safe.argtypes = [i32]
-    L.f5h_attn_force_safe.restype = ctypes.c_int
-    L.f5h_debug_tile_live.argtypes = [vp, i32, i32, i32, i32]
-    L.f5h_debug_tile_live.restype = ctypes.c_int
+    # test hooks: bound when present, so an older build loaded through F5H_LIB (one-box A/Bs) still loads
+    if hasattr(L, "f5h_attn_force_safe"):
+        L.f5h_attn_force_safe.argtypes = [i32]
+        L.f5h_attn_force_safe.restype = ctypes.c_int
+    if hasattr(L, "f5h_debug_tile_live"):
+        L.f5h_debug_tile_live.argtypes = [vp, i32, i32, i32, i32]
+        L.f5h_debug_tile_live.restype = ctypes.c_int
     L.f5h_vocos_create.argtypes = [ctypes.POINTER(VocosArch), ctypes.POINTER(Weight), i32, i32, ctypes.POINTER(vp)]
     L.f5h_vocos_create.restype = ctypes.c_int
     L.f5h_vocos_destroy.argtypes = [vp]
