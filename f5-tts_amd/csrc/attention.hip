@@ -74,7 +74,9 @@ F5H_DEV void attn_block(int& qb, int& bh) {
   bh = id / nqb;
 }
 
-template <typename T, bool PRESCALED, int NW>
+// RSM: row sums on the matrix pipe (l^T += ones . P^T, one 32x32x16 MFMA per 16-key chunk) instead of 16 packed
+// VALU adds per tile (F5H_ATTN_ROWSUM=mfma; an A/B switch, results agree to rounding)
+template <typename T, bool PRESCALED, int NW, bool RSM>
 __global__ __launch_bounds__(64 * NW, 8 / NW) void attn16_kernel(AttnArgs a) {
   typedef Op16<T> OP;
   typedef typename OP::v8 v8;
@@ -162,6 +164,12 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn16_kernel(AttnArgs a) {
   float m_run = 0.f;  // running max (log2 units), valid after tile 0
   f32x16 oacc[2], minit;  // minit: -m_run in every slot, the QK^T chains' first C operand
   f2 lrow = {0.f, 0.f};   // this lane's part of its query's row sum (packed fp32 adds)
+  f32x16 lacc;            // RSM: the row sums on the matrix pipe (every slot of a lane holds its query's sum)
+#pragma unroll
+  for (int r = 0; r < 16; ++r) lacc[r] = 0.f;
+  v8 ones;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) ones[j] = from_f32<T>(1.f);
 #pragma unroll
   for (int r = 0; r < 16; ++r) {
     oacc[0][r] = 0.f;
@@ -304,6 +312,10 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn16_kernel(AttnArgs a) {
 #pragma unroll
           for (int r = 0; r < 16; ++r) sacc[t][r] -= d;
         lrow *= alpha;
+        if constexpr (RSM) {
+#pragma unroll
+          for (int r = 0; r < 16; ++r) lacc[r] *= alpha;
+        }
       }
     }
     // exp2 / pack of 16-key chunk c = (t, sx) of P (row sums from the fp32 exp2s, four packed
@@ -318,7 +330,7 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn16_kernel(AttnArgs a) {
         const f2 e = {__builtin_amdgcn_exp2f(sacc[t][8 * sx + j]), __builtin_amdgcn_exp2f(sacc[t][8 * sx + j + 1])};
         pf[t][sx][j] = from_f32<T>(e.x);
         pf[t][sx][j + 1] = from_f32<T>(e.y);
-        lrow += e;
+        if constexpr (!RSM) lrow += e;
       }
     };
     auto mma_chunk = [&](auto C) {
@@ -328,6 +340,7 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn16_kernel(AttnArgs a) {
         const uint4 w = make_uint4(vf[u][t][sx][0].x, vf[u][t][sx][0].y, vf[u][t][sx][1].x, vf[u][t][sx][1].y);
         oacc[u] = OP::mma32(__builtin_bit_cast(v8, w), pf[t][sx], oacc[u]);
       }
+      if constexpr (RSM) lacc = OP::mma32(ones, pf[t][sx], lacc);
     };
     exp_chunk(std::integral_constant<int, 0>{});
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -384,8 +397,12 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn16_kernel(AttnArgs a) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no LDS-DMA outlives the loop (ntile == 0 included)
   };
   pass(IF{});
-  float l_tot = lrow.x + lrow.y;
-  l_tot += xor32(l_tot);  // lanes l and l + 32 hold the two key halves of one query
+  auto row_sum = [&]() -> float {
+    if constexpr (RSM) return lacc[0];  // D[m][n] = sum_k P[n][k] for every m: lanes l and l + 32 alike
+    float l = lrow.x + lrow.y;
+    return l + xor32(l);  // lanes l and l + 32 hold the two key halves of one query
+  };
+  float l_tot = row_sum();
   {
     // Did any row of the workgroup exceed LMAX (or overflow)? One word per wave in the ring's first bytes
     // (all reads of the last tile retired: every wave waited for its LDS reads before its last MFMAs).
@@ -404,6 +421,8 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn16_kernel(AttnArgs a) {
       m_run = 0.f;
       lrow = f2{0.f, 0.f};
 #pragma unroll
+      for (int r = 0; r < 16; ++r) lacc[r] = 0.f;
+#pragma unroll
       for (int r = 0; r < 16; ++r) {
         oacc[0][r] = 0.f;
         oacc[1][r] = 0.f;
@@ -413,8 +432,7 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn16_kernel(AttnArgs a) {
       dma(1, 1);
       dma(2, 2);
       pass(IT{});
-      l_tot = lrow.x + lrow.y;
-      l_tot += xor32(l_tot);
+      l_tot = row_sum();
     }
   }
   probe_mark(a.probe, probe_t, 2);
@@ -513,10 +531,18 @@ template <typename T>
 static void launch16(const AttnArgs& a, hipStream_t st) {
   constexpr int NW = 8;  // (two 4-wave workgroups per CU measured 40.3 vs 39.6 us at C2: kept one of 8)
   dim3 grid((a.L + 32 * NW - 1) / (32 * NW), a.S * a.H);
-  if (a.prescaled)
-    hipLaunchKernelGGL((attn16_kernel<T, true, NW>), grid, dim3(64 * NW), 0, st, a);
-  else
-    hipLaunchKernelGGL((attn16_kernel<T, false, NW>), grid, dim3(64 * NW), 0, st, a);
+  static const bool rsm = [] {
+    const char* v = getenv("F5H_ATTN_ROWSUM");
+    return v && !strcmp(v, "mfma");
+  }();
+  if (a.prescaled) {
+    if (rsm)
+      hipLaunchKernelGGL((attn16_kernel<T, true, NW, true>), grid, dim3(64 * NW), 0, st, a);
+    else
+      hipLaunchKernelGGL((attn16_kernel<T, true, NW, false>), grid, dim3(64 * NW), 0, st, a);
+  } else {
+    hipLaunchKernelGGL((attn16_kernel<T, false, NW, false>), grid, dim3(64 * NW), 0, st, a);
+  }
 }
 
 static int g_force_safe = 0;
