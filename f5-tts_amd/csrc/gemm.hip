@@ -14,13 +14,28 @@ static int gemm_env_cfg() {
 }
 
 
-// The 256x256 configuration of the large batches: 11 (ping-pong) or 12 (8-phase); env F5H_LARGE_CFG.
+// The 256x256 configuration of the large batches: 11 (ping-pong), 12 (8-phase) or 13 (persistent ping-pong);
+// env F5H_LARGE_CFG.
 static int large_cfg() {
   static const int v = [] {
     const char* e = getenv("F5H_LARGE_CFG");
-    return (e && atoi(e) == 12) ? 12 : 11;
+    const int c = e ? atoi(e) : 11;
+    return (c == 12 || c == 13) ? c : 11;
   }();
   return v;
+}
+
+// compute units of the current device (the persistent kernel's grid), cached per device
+int gemm_num_cus() {
+  static int cus[64] = {0};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
+  if (!cus[dev]) {
+    int n = 0;
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
+    cus[dev] = n;
+  }
+  return cus[dev];
 }
 
 // Tile choice for a bf16 GEMM among the 2-blocks-per-CU configurations 0, 1, 5: time ~

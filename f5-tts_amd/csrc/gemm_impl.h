@@ -988,6 +988,195 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(GemmArgs g) {
 }
 
 // ======================================================================================
+// Persistent ping-pong GEMM (cfg 13; whole-column tiles with the direct epilogue only): the gemm_pp_kernel
+// schedule, but one block per CU walks a sequence of tiles and the LDS-DMA pipeline runs across tile
+// boundaries -- the next tile's first phases are issued while the current tile's last phases compute, and its
+// operands land while the register-only epilogue runs -- so no tile pays a ramp, and no block-dispatch gap
+// separates a CU's tiles (profiles/archive/r03_timeline_c3_epilogue.txt: ~3 us between a CU's consecutive
+// 256x256 tiles beside a 2 us ramp). Tile order: XCD x (blocks b with b % 8 == x) takes the contiguous run of
+// n-fastest tiles the non-persistent remap gives it, its blocks dealt round-robin over the run, so an XCD's
+// resident tiles share A panels in its L2. Each accumulator takes its k-slabs in the same order as every other
+// configuration (bitwise identical results).
+// ======================================================================================
+template <typename TC, int EPI, int BM, int BN, int WGM2, int WGN2, int KS, int D>
+__global__ __launch_bounds__(512, 1) void gemm_ppp_kernel(GemmArgs g) {
+  const ProbeT probe_t = probe_enter(g.probe);
+  typedef PPCfg<BM, BN, WGM2, WGN2, KS, D> C;
+  constexpr int WM = C::WM, WN = C::WN, MT = C::MT, NT = C::NT, NA = C::NA, NB = C::NB;
+  constexpr int SB = C::stage_bytes, PB = KS * SB;  // stage / phase bytes
+  __shared__ __attribute__((aligned(16))) uint4 lds[C::ring_bytes / 16];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int grp = wid >> 2, w4 = wid & 3;
+  const int wm = w4 / WGN2, wn = w4 % WGN2;
+  const int ntn = (g.N + BN - 1) / BN, nmt = (g.M + BM - 1) / BM, T = nmt * ntn;
+  // this block's run: XCD x's contiguous tile range, every nbx-th tile from the block's position in it
+  const int nwg = gridDim.x, b = blockIdx.x, x = b & 7, j0 = b >> 3;
+  const int nbx = (nwg - x + 7) >> 3;  // blocks of this XCD
+  const int xq = T >> 3, xr = T & 7;
+  const int run0 = x < xr ? x * (xq + 1) : xr * (xq + 1) + (x - xr) * xq;
+  const int runn = xq + (x < xr ? 1 : 0);
+  // the k-th tile of the block (sequence index k >= 0): its (m0, n0), or false past the run's end; dead tiles
+  // (every row padding, RESID with live_len) are skipped by next_live
+  auto tile_of = [&](int k, int& m0, int& n0) -> bool {
+    const int r = j0 + k * nbx;
+    if (r >= runn) return false;
+    const int id = run0 + r;
+    const int mrow = g.live_len ? spread8(id / ntn, nmt) : id / ntn;
+    m0 = mrow * BM;
+    n0 = (id % ntn) * BN;
+    return true;
+  };
+  auto next_live = [&](int k, int& m0, int& n0) -> int {  // the first live tile at or after k, or -1
+    for (;; ++k) {
+      if (!tile_of(k, m0, n0)) return -1;
+      if constexpr (EPI == EPI_RESID || EPI == EPI_RESID16) {
+        if (!tile_live(g, m0, BM)) continue;
+      }
+      return k;
+    }
+  };
+  const TC* A = reinterpret_cast<const TC*>(g.A);
+  const TC* W = reinterpret_cast<const TC*>(g.W);
+
+  // ---- DMA (as gemm_pp_kernel): group 0 stages A rows, group 1 W rows; per tile the panel base and extent
+  constexpr int NI = NA > NB ? NA : NB;
+  const int nI = grp == 0 ? NA : NB;
+  const int ld = grp == 0 ? g.lda : g.ldw;
+  uint32_t voff[NI], dst_off[NI];
+#pragma unroll
+  for (int i = 0; i < NI; ++i) {
+    const int row = (i * 4 + w4) * 16 + (lane >> 2);
+    const int lc = swz64(row, lane & 3);
+    voff[i] = (uint32_t)((row * ld + lc * 8) * 2);
+    dst_off[i] = (uint32_t)((grp == 0 ? 0 : BM * 64) + (i * 4 + w4) * 16 * 64);
+  }
+  char* lds_c = reinterpret_cast<char*>(lds);
+  const int nph = g.K / (32 * KS);
+  // DMA cursor: tile dk (its m0/n0 in dm0/dn0), phase dp within it; gi = phases issued so far
+  int dm0 = 0, dn0 = 0;
+  int dk = next_live(0, dm0, dn0), dp = 0, gi = 0;
+  auto issue = [&]() {  // this wave's part of the next phase in the block's sequence, into ring slot gi % R
+    const int slot = gi % C::R;
+    const TC* pan = grp == 0 ? A + (int64_t)dm0 * g.lda : W + (int64_t)dn0 * g.ldw;
+    const TC* pan2 = (grp == 0 && g.A2) ? reinterpret_cast<const TC*>(g.A2) + (int64_t)dm0 * g.lda : pan;
+    const uint32_t pbytes = (uint32_t)((grp == 0 ? min(BM, g.M - dm0) : min(BN, g.N - dn0)) * ld * 2);
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+      const int k0 = (dp * KS + s) * 32;
+      const bool second = grp == 0 && g.A2 && k0 >= g.k_split;
+      const __amdgpu_buffer_rsrc_t rs = rsrc_of(second ? pan2 : pan, pbytes);
+      const int ks = second ? k0 - g.k_split : k0;
+#pragma unroll
+      for (int i = 0; i < NI; ++i)
+        if (i < nI) dma16(rs, (LDS_PTR(void))(lds_c + slot * PB + s * SB + dst_off[i]), voff[i], ks * 2);
+    }
+    ++gi;
+    if (++dp == nph) {
+      dp = 0;
+      dk = next_live(dk + 1, dm0, dn0);
+    }
+  };
+  auto wait_dma = [&](int need, int issued) {  // own DMA of global phase `need` landed (younger ones in flight)
+    const int younger = min(max(issued - need, 0), D - 1);
+    static_for<0, D>([&](auto Y) {
+      constexpr int y = decltype(Y)::value;
+      if (younger == y) {
+        if (grp == 0)
+          asm volatile("s_waitcnt vmcnt(%0)" ::"i"(y * KS * NA) : "memory");
+        else
+          asm volatile("s_waitcnt vmcnt(%0)" ::"i"(y * KS * NB) : "memory");
+      }
+    });
+  };
+
+  const uint32_t lds0 = (uint32_t)(uintptr_t)(LDS_PTR(void))lds;
+  const int fr = lane & 15, q = lane >> 4;
+  const int arow = grp * (BM / 2) + wm * WM + fr, brow = wn * WN + fr;
+  const uint32_t a_lane = lds0 + arow * 64 + swz64(arow, q) * 16;
+  const uint32_t b_lane = lds0 + BM * 64 + brow * 64 + swz64(brow, q) * 16;
+
+  f32x4 acc[MT][NT];
+#pragma unroll
+  for (int i = 0; i < MT; ++i)
+#pragma unroll
+    for (int j = 0; j < NT; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  u32x4 af[KS][MT], bfr[KS][NT];
+  auto read_phase = [&](int gp) {
+    const uint32_t so = (uint32_t)((gp % C::R) * PB);
+    static_for<0, KS>([&](auto S) {
+      constexpr int s = decltype(S)::value;
+      static_for<0, MT>([&](auto I) {
+        constexpr int i = decltype(I)::value;
+        af[s][i] = lds_read_b128<s * SB + i * 1024>(a_lane + so);
+      });
+      static_for<0, NT>([&](auto J) {
+        constexpr int j = decltype(J)::value;
+        bfr[s][j] = lds_read_b128<s * SB + j * 1024>(b_lane + so);
+      });
+    });
+  };
+
+  // compute cursor: tile ck (its m0/n0), phase cp within it; gc = global phase index
+  int cm0 = 0, cn0 = 0;
+  int ck = next_live(0, cm0, cn0), cp = 0, gc = 0;
+  if (ck < 0) {  // no live tile for this block
+    probe_exit(g.probe, probe_t);
+    return;
+  }
+  for (int p = 0; p < D && dk >= 0; ++p) issue();
+  wait_dma(0, gi - 1);
+  __builtin_amdgcn_s_barrier();
+  if (grp == 1) __builtin_amdgcn_s_barrier();  // group 1 sits out half-period 0
+  const V8 none[1][1] = {};
+  for (;;) {
+    // ---- mem(gc): fragments of phase gc, DMA of phase gc + D (possibly the next tile's), own part of gc + 1
+    read_phase(gc);
+    if (dk >= 0) issue();
+    wait_dma(gc + 1, gi - 1);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+#pragma unroll
+      for (int i = 0; i < MT; ++i) asm volatile("" : "+v"(af[s][i]));
+#pragma unroll
+      for (int j = 0; j < NT; ++j) asm volatile("" : "+v"(bfr[s][j]));
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    // ---- mma(gc)
+    typedef typename Op16<TC>::v8 v8;
+#pragma unroll
+    for (int s = 0; s < KS; ++s)
+#pragma unroll
+      for (int i = 0; i < MT; ++i)
+#pragma unroll
+        for (int j = 0; j < NT; ++j)
+          acc[i][j] = Op16<TC>::mma16(__builtin_bit_cast(v8, bfr[s][j]), __builtin_bit_cast(v8, af[s][i]), acc[i][j]);
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    ++gc;
+    if (++cp == nph) {
+      // the tile's epilogue (registers and global memory only: the ring keeps filling with the next tile)
+      epilogue_direct<TC, EPI, MT, NT, false>(g, acc, cm0 + grp * (BM / 2) + wm * WM, cn0 + wn * WN, lane, none);
+#pragma unroll
+      for (int i = 0; i < MT; ++i)
+#pragma unroll
+        for (int j = 0; j < NT; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+      cp = 0;
+      ck = next_live(ck + 1, cm0, cn0);
+      if (ck < 0) break;
+    }
+  }
+  if (grp == 0) __builtin_amdgcn_s_barrier();  // matches group 1's extra barrier
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  probe_exit(g.probe, probe_t);
+}
+
+// ======================================================================================
 // 256x256 8-phase GEMM (16-bit operands; cdna_hip_programming.md §5, "The 256² 8-phase template"):
 // 512 threads = 8 waves, one block per CU. K-tiles of 64 alternate between two 64 KB LDS buffers; a
 // buffer holds the tile's A rows [0,256) and W rows [0,256) as four 128-row halves (A-top, A-bottom,
@@ -1253,6 +1442,23 @@ static void launch_pp(const GemmArgs& a, hipStream_t st) {
   hipLaunchKernelGGL((gemm_pp_kernel<TC, EPI, BM, BN, WGM2, WGN2, KS, D>), dim3(tiles), dim3(512), 0, st, a);
 }
 
+// cfg 13: one persistent block per CU (whole-column tiles with the direct epilogue; others take cfg 11)
+int gemm_num_cus();
+template <typename TC, int EPI, int BM, int BN, int WGM2, int WGN2, int KS, int D>
+static void launch_ppp(const GemmArgs& a, hipStream_t st) {
+  const int tiles = ((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN);
+  constexpr bool HOT = EPI == EPI_QKV || EPI == EPI_RESID || EPI == EPI_RESID16 || EPI == EPI_GELU_TANH ||
+                       EPI == EPI_GELU_ERF_OP || EPI == EPI_STORE || EPI == EPI_STORE16 || EPI == EPI_INPROJ;
+  if constexpr (HOT) {
+    if (fast_epi_ok<EPI>(a, BN) && a.K >= 32 * KS * D) {
+      const int grid = std::min(tiles, gemm_num_cus());
+      hipLaunchKernelGGL((gemm_ppp_kernel<TC, EPI, BM, BN, WGM2, WGN2, KS, D>), dim3(grid), dim3(512), 0, st, a);
+      return;
+    }
+  }
+  launch_pp<TC, EPI, BM, BN, WGM2, WGN2, KS, D>(a, st);
+}
+
 // Tile configurations (16-bit operands; the fp32 parity mode always uses cfg 0):
 //   0: 64x128,  4 waves (2x2, 32x64 each),  3 stages, 2 blocks/CU
 //   1: 128x128, 4 waves (2x2, 64x64 each),  2 stages, 2 blocks/CU
@@ -1303,9 +1509,11 @@ static hipError_t launch_t(const GemmArgs& a, hipStream_t st) {
     case 5: launch_cfg<TC, EPI, 192, 128, 2, 2, 2>(a, st); break;
     default:
       if constexpr (is16<TC>()) {
-        if ((cfg != 11 && cfg != 12) || a.K % 64) return hipErrorInvalidValue;  // whole K64 tiles
+        if ((cfg != 11 && cfg != 12 && cfg != 13) || a.K % 64) return hipErrorInvalidValue;  // whole K64 tiles
         if (cfg == 11)
           launch_pp<TC, EPI, 256, 256, 1, 4, 1, 3>(a, st);
+        else if (cfg == 13)
+          launch_ppp<TC, EPI, 256, 256, 1, 4, 1, 3>(a, st);
         else
           launch_8p<TC, EPI>(a, st);
         break;

@@ -67,7 +67,7 @@ def test_op_linear(compute, tol, M, N, K):
     assert err < tol, err
 
 
-GEMM_CONFIGS = [0, 1, 5, 11, 12]  # 11: ping-pong 8-wave 256x256 kernel; 12: 8-phase 256x256 kernel
+GEMM_CONFIGS = [0, 1, 5, 11, 12, 13]  # 11: ping-pong 8-wave 256x256; 12: 8-phase 256x256; 13: persistent ping-pong
 if os.environ.get("F5H_TEST_GEMM_CFGS"):  # tuning runs: check extra configurations too
     GEMM_CONFIGS = [int(c) for c in os.environ["F5H_TEST_GEMM_CFGS"].split(",")]
 
