@@ -20,7 +20,8 @@ SHAPES = {  # name: (M, N, K); C2 = 2 x 1876 rows, C3 = 64 x 1876 rows
 for _k in (128, 256, 512, 2048, 4096):  # K sweeps at the C2 output shapes: fixed cost per launch = intercept
     SHAPES[f"c2_out_k{_k}"] = (3752, 1024, _k)
     SHAPES[f"c2_qkv_k{_k}"] = (3752, 3072, _k)
-CFGS = {0: (64, 128, 256), 1: (128, 128, 256), 5: (192, 128, 256), 11: (256, 256, 512), 12: (256, 256, 512)}
+CFGS = {0: (64, 128, 256), 1: (128, 128, 256), 5: (192, 128, 256), 11: (256, 256, 512), 12: (256, 256, 512),
+        13: (256, 256, 512)}  # 13: persistent (one block per CU)
 # round 3 also timed register-staged intake (cfg 40-45) and K32-stage deeper rings for 192x128 / 128x128
 # (cfg 6-8): slower on every C2 and C3 shape (profiles/r03_gemm_tune_rs_c2.txt, r03_gemm_tune_k32.txt)
 # round 2 also timed 8-wave one-block-per-CU tiles (128x256, 192x256, 256x128, 128x128, 256x256, 256x192),
@@ -35,7 +36,8 @@ if os.environ.get("GT_SHAPES"):
 
 def grid_threads(M, N, cfg):
     bm, bn, th = CFGS[cfg]
-    return ((M + bm - 1) // bm) * ((N + bn - 1) // bn) * th
+    tiles = ((M + bm - 1) // bm) * ((N + bn - 1) // bn)
+    return (min(tiles, 256) if cfg == 13 else tiles) * th
 
 
 ROUNDS, PER = 5, REPS // 5  # interleaved rounds per shape (MI355X_MICROARCH DVFS: compare within one process)
