@@ -25,6 +25,16 @@ static int large_cfg() {
   return v;
 }
 
+// the persistent kernel's tile grouping (F5H_GEMM_GROUP_M, default 1: n-fastest, the non-persistent order)
+int gemm_group_m() {
+  static const int v = [] {
+    const char* e = getenv("F5H_GEMM_GROUP_M");
+    const int g = e ? atoi(e) : 1;
+    return g > 1 && g <= 64 ? g : 1;
+  }();
+  return v;
+}
+
 // compute units of the current device (the persistent kernel's grid), cached per device
 int gemm_num_cus() {
   static int cus[64] = {0};

@@ -1019,13 +1019,27 @@ __global__ __launch_bounds__(512, 1) void gemm_ppp_kernel(GemmArgs g) {
   const int runn = xq + (x < xr ? 1 : 0);
   // the k-th tile of the block (sequence index k >= 0): its (m0, n0), or false past the run's end; dead tiles
   // (every row padding, RESID with live_len) are skipped by next_live
+  // GM > 1 (F5H_GEMM_GROUP_M): tile ids run m-fastest inside groups of GM row tiles, so the nbx tiles an XCD
+  // holds at once form a GM x (nbx / GM) block (e.g. 4 x 8) that shares both A and W panels in its L2, instead
+  // of ~3 rows x every column (the W panels of all columns re-streamed per wave of tiles)
+  const int GM = g.group_m > 1 ? g.group_m : 1;
   auto tile_of = [&](int k, int& m0, int& n0) -> bool {
     const int r = j0 + k * nbx;
     if (r >= runn) return false;
     const int id = run0 + r;
-    const int mrow = g.live_len ? spread8(id / ntn, nmt) : id / ntn;
+    int mt, nt;
+    if (GM > 1) {
+      const int gsz = GM * ntn, grp0 = id / gsz, in = id - grp0 * gsz;
+      const int gm = min(GM, nmt - grp0 * GM);  // rows in this (possibly partial, last) group
+      mt = grp0 * GM + in % gm;
+      nt = in / gm;
+    } else {
+      mt = id / ntn;
+      nt = id % ntn;
+    }
+    const int mrow = g.live_len ? spread8(mt, nmt) : mt;
     m0 = mrow * BM;
-    n0 = (id % ntn) * BN;
+    n0 = nt * BN;
     return true;
   };
   auto next_live = [&](int k, int& m0, int& n0) -> int {  // the first live tile at or after k, or -1
@@ -1444,6 +1458,7 @@ static void launch_pp(const GemmArgs& a, hipStream_t st) {
 
 // cfg 13: one persistent block per CU (whole-column tiles with the direct epilogue; others take cfg 11)
 int gemm_num_cus();
+int gemm_group_m();
 template <typename TC, int EPI, int BM, int BN, int WGM2, int WGN2, int KS, int D>
 static void launch_ppp(const GemmArgs& a, hipStream_t st) {
   const int tiles = ((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN);
@@ -1452,7 +1467,9 @@ static void launch_ppp(const GemmArgs& a, hipStream_t st) {
   if constexpr (HOT) {
     if (fast_epi_ok<EPI>(a, BN) && a.K >= 32 * KS * D) {
       const int grid = std::min(tiles, gemm_num_cus());
-      hipLaunchKernelGGL((gemm_ppp_kernel<TC, EPI, BM, BN, WGM2, WGN2, KS, D>), dim3(grid), dim3(512), 0, st, a);
+      GemmArgs b = a;
+      b.group_m = gemm_group_m();
+      hipLaunchKernelGGL((gemm_ppp_kernel<TC, EPI, BM, BN, WGM2, WGN2, KS, D>), dim3(grid), dim3(512), 0, st, b);
       return;
     }
   }

@@ -65,6 +65,7 @@ struct GemmArgs {
   // live_len[s]); a tile with no live row skips its K loop and epilogue (its rows keep the residual, as
   // the masked rows of a computed tile do). Null: every tile is computed.
   const int32_t* live_len; int live_seq;
+  int group_m;                     // persistent kernel (cfg 13): tile order in groups of this many row tiles (<= 1: n-fastest)
 };
 
 // Does the row tile [m0, m0 + BM) of an M-row GEMM hold a live row? Sequence s (rows [s*live_seq, (s+1)*live_seq))
