@@ -5,7 +5,7 @@
 # with empty kernels), so each pass makes 3 calls (~8k dispatches): 1 warm + 2 marked.
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"; export TMPDIR=/tmp F5H_TRACE_WARM=1 F5H_TRACE_CALLS=2
-O=$PWD/gpurun_out/pmc_c2; mkdir -p $O
+O=$PWD/gpurun_out/pmc_${2:-c2}; mkdir -p $O
 OUT=${1:-$O/r03_pmc_classes.json}
 CFG=${2:-c2}
 # C3/C4/C5: graph-mode passes at the batch shapes never finish under the profiler (tools/r04_gpu_a.sh,
