@@ -97,3 +97,22 @@ def test_fp16_gemm_epilogues_round_through_fp32(tmp_path):
         elif cur and "v_fma_mix" in ln:
             mixed.add(cur)
     assert kernels >= 10 and not mixed, (kernels, sorted(mixed))
+
+
+@pytest.mark.parametrize("src", ["attention.hip", "gemm_bf16_a.hip"])
+def test_lds_dma_never_in_a_waterfall_loop(src, tmp_path):
+    """Every LDS-DMA piece (`buffer_load_dwordx4 ... lds`) takes its buffer descriptor from scalar registers the
+    compiler can prove wave-uniform. A descriptor it cannot (e.g. an extent computed on the VALU) makes hipcc wrap
+    each piece in a waterfall loop: v_readfirstlane x4, a compare, s_and_saveexec, the load, s_xor exec, branch
+    back (cdna_hip_programming.md T20; round 5's per-tile attention descriptors did this until the extent went
+    through readfirstlane)."""
+    lines = [ln.strip() for ln in _asm(src, tmp_path)]
+    dma = [i for i, ln in enumerate(lines) if ln.startswith("buffer_load_dwordx4") and ln.endswith(" lds")]
+    assert len(dma) > 10, len(dma)
+    bad = []
+    for i in dma:
+        window = lines[max(0, i - 8):i]
+        if any(w.startswith("s_and_saveexec") for w in window) or \
+                sum(w.startswith("v_readfirstlane_b32") for w in window) >= 4:
+            bad.append((i, lines[i]))
+    assert not bad, bad[:5]
