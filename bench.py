@@ -424,19 +424,47 @@ def _free_port():
     return port
 
 
-def visible_gpus():
-    """GPUs a rank process would see, counted in a child process: the launcher's own process makes no HIP
-    call at all (torch.cuda.device_count() can fall back to hipGetDeviceCount when amdsmi cannot initialise,
-    which starts the HIP runtime in the parent of the ranks)."""
-    import subprocess
-
-    code = "import torch; print(torch.cuda.device_count())"
+def kfd_gpu_nodes(root="/sys/class/kfd/kfd/topology/nodes"):
+    """Physical GPUs from the KFD topology in sysfs (nodes whose properties list `simd_count > 0`; CPU nodes
+    have 0). Pure file reads, no HIP call. None when the topology is unreadable."""
     try:
-        out = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=300,
-                             env=dict(os.environ))
-        return int(out.stdout.strip().splitlines()[-1])
-    except (subprocess.SubprocessError, ValueError, IndexError):
-        return 0
+        names = os.listdir(root)
+    except OSError:
+        return None
+    n = 0
+    for d in names:
+        try:
+            with open(os.path.join(root, d, "properties")) as f:
+                props = dict(ln.split(None, 1) for ln in f if len(ln.split(None, 1)) == 2)
+        except OSError:
+            continue
+        if int(props.get("simd_count", "0").strip() or 0) > 0:
+            n += 1
+    return n
+
+
+def visible_gpus(root="/sys/class/kfd/kfd/topology/nodes"):
+    """GPUs a rank process would see, counted without any HIP call in the launcher's process
+    (torch.cuda.device_count() can fall back to hipGetDeviceCount when amdsmi cannot initialise, which starts
+    the HIP runtime in the parent of the ranks): the KFD topology in sysfs, narrowed by ROCR_VISIBLE_DEVICES
+    and then HIP_VISIBLE_DEVICES / CUDA_VISIBLE_DEVICES the way the runtime applies them. Only if sysfs is
+    unreadable is the count taken from a child process."""
+    n = kfd_gpu_nodes(root)
+    if n is None:
+        import subprocess
+
+        code = "import torch; print(torch.cuda.device_count())"
+        try:
+            out = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=300,
+                                 env=dict(os.environ))
+            return int(out.stdout.strip().splitlines()[-1])
+        except (subprocess.SubprocessError, ValueError, IndexError):
+            return 0
+    for var in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        v = os.environ.get(var)
+        if v is not None:
+            n = min(n, len([x for x in v.split(",") if x.strip()]))
+    return n
 
 
 def launch_ranks(args, argv):

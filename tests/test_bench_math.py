@@ -260,3 +260,20 @@ def test_live_row_traffic_pricing_at_c3(fake_profiles):
     assert out["algorithmic_bytes"] == 2 * (sum(q) * 1024 + 1024 * 1024) + 2 * 2 * sum(q) * 1024
     for e in (at, out):
         assert e["traffic"] and 0.95 < e["traffic_over_algorithmic"] < 2.0
+
+
+def test_visible_gpus_reads_kfd_topology(tmp_path, monkeypatch):
+    """The launcher's GPU count comes from sysfs (KFD nodes with SIMDs) narrowed by the visibility variables;
+    no torch/HIP entry is reached."""
+    for i, simds in enumerate([0, 1024, 1024, 0, 1024]):
+        (tmp_path / str(i)).mkdir()
+        (tmp_path / str(i) / "properties").write_text(f"cpu_cores_count 4\nsimd_count {simds}\nmax_waves_per_simd 8\n")
+    for var in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        monkeypatch.delenv(var, raising=False)
+    assert bench.kfd_gpu_nodes(str(tmp_path)) == 3
+    assert bench.visible_gpus(str(tmp_path)) == 3
+    monkeypatch.setenv("HIP_VISIBLE_DEVICES", "0,2")
+    assert bench.visible_gpus(str(tmp_path)) == 2
+    monkeypatch.setenv("ROCR_VISIBLE_DEVICES", "1")
+    assert bench.visible_gpus(str(tmp_path)) == 1
+    assert bench.kfd_gpu_nodes(str(tmp_path / "absent")) is None
