@@ -166,51 +166,27 @@ __global__ __launch_bounds__(256) void ln_mod_kernel(const TI* h, int M, int d, 
 template <typename T>
 __global__ __launch_bounds__(256) void ln_mod16_kernel(const T* h, int M, const float* shift, const float* scale,
                                                        T* out) {
-  typedef typename Op16<T>::v8 v8;
   constexpr int d = 1024;
   const int row = xcd_block(blockIdx.x, gridDim.x) * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
   if (row >= M) return;
   const uint4* x = reinterpret_cast<const uint4*>(h + (int64_t)row * d);
   const float4* sh = reinterpret_cast<const float4*>(shift);
   const float4* sc = reinterpret_cast<const float4*>(scale);
-  float v[2][8];
+  uint4 xv[2], o[2];
   float4 a[2][2], b[2][2];
 #pragma unroll
   for (int k = 0; k < 2; ++k) {
     const int c = lane + 64 * k;
-    const v8 w = __builtin_bit_cast(v8, x[c]);
-#pragma unroll
-    for (int e = 0; e < 8; ++e) v[k][e] = to_f32(w[e]);
+    xv[k] = x[c];
     a[k][0] = sc[2 * c];
     a[k][1] = sc[2 * c + 1];
     b[k][0] = sh[2 * c];
     b[k][1] = sh[2 * c + 1];
   }
-  float s = 0.f;
+  ln16_row<T>(xv, a, b, o);
+  uint4* op = reinterpret_cast<uint4*>(out + (int64_t)row * d);
 #pragma unroll
-  for (int k = 0; k < 2; ++k)
-#pragma unroll
-    for (int e = 0; e < 8; ++e) s += v[k][e];
-  const float mean = wave_sum_dpp(s) / d;
-  float q = 0.f;
-#pragma unroll
-  for (int k = 0; k < 2; ++k)
-#pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      const float p = v[k][e] - mean;
-      q += p * p;
-    }
-  const float rstd = rsqrtf(wave_sum_dpp(q) / d + 1e-6f);
-  uint4* o = reinterpret_cast<uint4*>(out + (int64_t)row * d);
-#pragma unroll
-  for (int k = 0; k < 2; ++k) {
-    const float av[8] = {a[k][0].x, a[k][0].y, a[k][0].z, a[k][0].w, a[k][1].x, a[k][1].y, a[k][1].z, a[k][1].w};
-    const float bv[8] = {b[k][0].x, b[k][0].y, b[k][0].z, b[k][0].w, b[k][1].x, b[k][1].y, b[k][1].z, b[k][1].w};
-    v8 w;
-#pragma unroll
-    for (int e = 0; e < 8; ++e) w[e] = from_f32<T>((v[k][e] - mean) * rstd * (1.f + av[e]) + bv[e]);
-    o[lane + 64 * k] = __builtin_bit_cast(uint4, w);
-  }
+  for (int k = 0; k < 2; ++k) op[lane + 64 * k] = o[k];
 }
 
 hipError_t ln_modulate(int compute, const void* hv, int h16, int M, int d, const float* shift, const float* scale,

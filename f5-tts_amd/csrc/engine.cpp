@@ -70,13 +70,13 @@ struct Layer {
 struct GraphKey {
   const void* ws;
   int kind;  // 0: one NFE step, 1: the call prologue (inputs staged into the workspace)
-  int B, N, nt, nfe, use_cfg, batch_mask, probe, split, pad_skip;
+  int B, N, nt, nfe, use_cfg, batch_mask, probe, split, pad_skip, chain;
   uint64_t kernel_epoch;  // bumped whenever a forced GEMM config changes
   uint32_t cfg_bits;
   bool operator==(const GraphKey& o) const {
     return ws == o.ws && kind == o.kind && B == o.B && N == o.N && nt == o.nt && nfe == o.nfe && kernel_epoch == o.kernel_epoch &&
            use_cfg == o.use_cfg && batch_mask == o.batch_mask && probe == o.probe && cfg_bits == o.cfg_bits &&
-           split == o.split && pad_skip == o.pad_skip;
+           split == o.split && pad_skip == o.pad_skip && chain == o.chain;
   }
 };
 
@@ -118,6 +118,9 @@ struct f5h_engine {
   // skip the dead pad-row work of the batch path (attention query blocks and out-proj row tiles of padding
   // only): f5h_set_pad_skip, env F5H_NO_PAD_SKIP=1 at creation turns it off. Bitwise identical results.
   int pad_skip = 1;
+  // In-launch phase chain of the DiT block-step's row-local seams (chain.hip): f5h_set_chain, env F5H_CHAIN=1 at
+  // creation. Bitwise identical results.
+  int chain = 0;
   uint64_t use_ctr = 0;
   int64_t n_captures = 0, n_replays = 0;
   // probe
@@ -464,6 +467,8 @@ struct Bufs {
   float2* rope;
   uint8_t* rowkeep;
   int32_t* kvlen;
+  unsigned* chain[2];  // phase-chain arrival counters per CFG part: [depth][5][chain_g4]
+  int chain_g4;        // row groups per counter row, rounded up to 4 (16-B rows)
   float *ada_cur, *temb_cur, *tgrid;  // the current step's table rows; device copy of the grid
   int* kstep;                         // device-side NFE step index
   float* y;                           // ODE state [B][N][mel] fp32
@@ -518,6 +523,9 @@ static void layout(const f5h_engine* e, WS& ws, Bufs& b, int B, int N, int nfe, 
   b.rope = ws.take<float2>((size_t)L * 32);
   b.rowkeep = ws.take<uint8_t>(rows);
   b.kvlen = ws.take<int32_t>(S);
+  b.chain_g4 = ((int)((rows + kChainRows - 1) / kChainRows) + 3) / 4 * 4;
+  for (int p = 0; p < 2; ++p)
+    b.chain[p] = a.backbone == F5H_DIT ? ws.take<unsigned>((size_t)a.depth * 5 * b.chain_g4) : nullptr;
   b.ada_cur = a.backbone == F5H_DIT ? ws.take<float>((size_t)e->ada.Npad) : nullptr;
   b.temb_cur = ws.take<float>((size_t)d);
   b.tgrid = ws.take<float>((size_t)nfe);
@@ -764,6 +772,27 @@ static int backbone_part(Ctx& c, int s0, int ns, hipStream_t st) {
   const int epi_resid = r16 ? EPI_RESID16 : EPI_RESID;
   void* h = bh;             // the layer's output (residual updates land here)
   const void* h_in = nullptr;  // UNetT first half: the layer input, kept as its skip connection
+  auto qkv_args = [&](const Layer& Lq) {
+    GemmArgs g = gargs(aop, d, Lq.qkv, rows, nullptr, 0);
+    g.rope = b.rope;
+    g.seq_len = c.L;
+    g.heads = H;
+    g.rope_heads = a.pe_attn_head > 0 ? a.pe_attn_head : H;
+    g.q = q;
+    g.k = k;
+    g.v = v;
+    g.q_scale = 0.125f * 1.4426950408889634f;  // softmax scale 1/sqrt(64) in log2 units, folded into q
+    return g;
+  };
+  // In-launch phase chain (chain.hip): a layer's out-proj .. FFN2 plus the next layer's LayerNorm + QKV (or
+  // the final LayerNorm) as one launch. The 16-bit DiT path without row masks (single-utterance calls); not
+  // while a chained class is probed (its launches are timed one by one).
+  const int part = s0 ? 1 : 0;
+  const bool chain_on = dit && r16 && do_ln && e->chain && !keep && d == 1024 && b.chain[part] &&
+                        (e->probe_class < 0 || e->probe_class == KC_ATTN || e->probe_class == KC_CONV);
+  if (chain_on) KCK(hipMemsetAsync(b.chain[part], 0, (size_t)a.depth * 5 * b.chain_g4 * sizeof(unsigned), st));
+  bool qkv_done = false;    // this layer's LayerNorm + QKV came with the previous layer's chain
+  bool final_done = false;  // the final LayerNorm came with the last layer's chain
   for (int l = 0; l < a.depth; ++l) {
     Layer& Ly = e->layers[l];
     const float* ad = ada_k ? ada_k + (size_t)l * 6 * d : nullptr;
@@ -788,21 +817,14 @@ static int backbone_part(Ctx& c, int s0, int ns, hipStream_t st) {
         KCK(rms_norm_g(bf, h, r16, rows, d, Ly.g_attn, aop, st));
       }
     } else {
-      if (do_ln) KCK(ln_modulate(bf, h, r16, rows, d, ad /*shift_msa*/, ad + d /*scale_msa*/, aop, st));
+      if (do_ln && !qkv_done) KCK(ln_modulate(bf, h, r16, rows, d, ad /*shift_msa*/, ad + d /*scale_msa*/, aop, st));
     }
-    {
-      GemmArgs g = gargs(aop, d, Ly.qkv, rows, nullptr, 0);
-      g.rope = b.rope;
-      g.seq_len = c.L;
-      g.heads = H;
-      g.rope_heads = a.pe_attn_head > 0 ? a.pe_attn_head : H;
-      g.q = q;
-      g.k = k;
-      g.v = v;
-      g.q_scale = 0.125f * 1.4426950408889634f;  // softmax scale 1/sqrt(64) in log2 units, folded into q
+    if (!qkv_done) {
+      GemmArgs g = qkv_args(Ly);
       ProbeScope ps(e, KC_QKV, st, &c.site, &g.probe);
       KCK(gemm(bf, EPI_QKV, g, st));
     }
+    qkv_done = false;
     {
       AttnArgs at{};
       at.q = q;
@@ -819,6 +841,32 @@ static int backbone_part(Ctx& c, int s0, int ns, hipStream_t st) {
       at.prescaled = 1;
       ProbeScope ps(e, KC_ATTN, st, &c.site, &at.probe);
       KCK(attention(bf, at, st));
+    }
+    if (chain_on) {
+      ChainArgs ca{};
+      ca.out = gargs(o, inner, Ly.out, rows, h, d);
+      ca.out.gate = ad + 2 * d;  // gate_msa
+      ca.ln1 = LnArgs{h, aop, ad + 3 * d /*shift_mlp*/, ad + 4 * d /*scale_mlp*/};
+      ca.ff1 = gargs(aop, d, Ly.ff1, rows, f, a.ff_dim);
+      ca.ff2 = gargs(f, a.ff_dim, Ly.ff2, rows, h, d);
+      ca.ff2.gate = ad + 5 * d;  // gate_mlp
+      if (l + 1 < a.depth) {
+        const float* an = ada_k + (size_t)(l + 1) * 6 * d;
+        ca.ln2 = LnArgs{h, aop, an /*shift_msa*/, an + d /*scale_msa*/};
+        ca.qkv = qkv_args(e->layers[l + 1]);
+      } else {
+        const float* fin = ada_k + (size_t)a.depth * 6 * d;  // AdaLayerNorm_Final: (scale, shift)
+        ca.ln2 = LnArgs{h, aop, fin + d, fin};
+      }
+      ca.cnt = b.chain[part] + (size_t)l * 5 * b.chain_g4;
+      ca.groups = (rows + kChainRows - 1) / kChainRows;
+      const hipError_t ce = chain_launch(bf, ca, st);
+      if (ce == hipSuccess) {
+        qkv_done = l + 1 < a.depth;
+        final_done = l + 1 == a.depth;
+        continue;
+      }
+      if (ce != hipErrorInvalidValue) KCK(ce);  // shapes outside the chain: the separate launches below
     }
     {
       GemmArgs g = gargs(o, inner, Ly.out, rows, h, d);
@@ -856,7 +904,7 @@ static int backbone_part(Ctx& c, int s0, int ns, hipStream_t st) {
   }
   if (dit) {
     const float* fin = ada_k + (size_t)a.depth * 6 * d;  // AdaLayerNorm_Final: (scale, shift)
-    KCK(ln_modulate(bf, h, r16, rows, d, fin + d, fin, aop, st));
+    if (!final_done) KCK(ln_modulate(bf, h, r16, rows, d, fin + d, fin, aop, st));
   } else {
     KCK(rms_norm_g(bf, h, r16, rows, d, e->norm_out_g, aop, st));
   }
@@ -935,6 +983,7 @@ int f5h_engine_create_views(const f5h_arch* arch, const f5h_tensor_view* weights
   if (const char* gv = getenv("F5H_GRAPH")) e->graph_mode = atoi(gv) ? 1 : 0;
   if (const char* sv = getenv("F5H_SPLIT_CFG")) e->split_cfg = std::min(2, std::max(0, atoi(sv)));
   if (const char* pv = getenv("F5H_NO_PAD_SKIP")) e->pad_skip = (*pv == '1') ? 0 : 1;
+  if (const char* cv = getenv("F5H_CHAIN")) e->chain = (*cv == '1') ? 1 : 0;
   // device views are read on the engine's non-blocking stream: order it behind the null stream (so behind
   // every blocking stream's queued work, the ordering the packing had when it ran on the null stream); work
   // on other non-blocking streams must be complete (f5h.h)
@@ -1211,6 +1260,7 @@ static int run_steps(Ctx& c, const f5h_sample_args* a, const void* ws) {
   const bool split = e->split_cfg == 1;  // auto (2): one packed chain
   key.split = split;
   key.pad_skip = e->pad_skip;
+  key.chain = e->chain;
   key.kernel_epoch = g_kernel_epoch.load();
   std::memcpy(&key.cfg_bits, &a->cfg_strength, 4);
   std::shared_ptr<GraphEntry> hold;  // keeps the replayed graph alive through the launch loop
@@ -1424,6 +1474,7 @@ int f5h_forward(f5h_engine* e, void* stream, const f5h_forward_args* a, void* wo
     key.batch_mask = c.batch_mask;
     key.probe = e->probe_class;
     key.pad_skip = e->pad_skip;
+    key.chain = e->chain;
     key.kernel_epoch = g_kernel_epoch.load();
     std::shared_ptr<GraphEntry> hold;
     RC(graph_get(c, key, false, body, hold, 1));
@@ -1516,6 +1567,24 @@ int f5h_set_pad_skip(f5h_engine* e, int32_t enable) {
   if (enable != 0 && enable != 1) return fail(F5H_EINVAL, "pad skip must be 0 or 1");
   std::lock_guard<std::mutex> g(e->gm);
   e->pad_skip = enable;
+  return 0;
+}
+
+int f5h_set_chain(f5h_engine* e, int32_t enable) {
+  if (!e) return fail(F5H_EINVAL, "null engine");
+  if (enable != 0 && enable != 1) return fail(F5H_EINVAL, "chain must be 0 or 1");
+  std::lock_guard<std::mutex> g(e->gm);
+  e->chain = enable;
+  return 0;
+}
+
+int f5h_chain_stats(int64_t* launches, int32_t* fault) {
+  if (launches) *launches = f5h::chain_launches();
+  if (fault) {
+    const int f = f5h::chain_fault_take();
+    if (f < 0) return fail(F5H_EHIP, "chain fault word unreadable");
+    *fault = f;
+  }
   return 0;
 }
 

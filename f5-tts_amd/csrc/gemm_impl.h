@@ -22,6 +22,7 @@
 #pragma once
 #include "common.h"
 #include "kernels.h"
+#include "chain.h"
 
 #include <cstdio>
 #include <cstdlib>
@@ -285,20 +286,22 @@ F5H_DEV void wait_stages(int n_stages) {
 
 // 16 bytes stored through a buffer descriptor: offsets past its extent are dropped by the hardware
 // range check, so out-of-range rows need no branch around the store
+// AUX: the cache-policy bits (kAuxWT: write-through, the in-launch hand-off's payload form)
+template <int AUX = 0>
 F5H_DEV void store16_rs(__amdgpu_buffer_rsrc_t r, uint32_t off, u32x4 v) {
-  __builtin_amdgcn_raw_buffer_store_b128(v, r, off, 0, 0);
+  __builtin_amdgcn_raw_buffer_store_b128(v, r, off, 0, AUX);
 }
-template <typename TC>
+template <typename TC, int AUX = 0>
 F5H_DEV void store8_rs(__amdgpu_buffer_rsrc_t r, uint32_t elem, const V8& x) {
   if constexpr (is16<TC>()) {
     typedef typename Op16<TC>::v8 v8;
     const v8 b = {from_f32<TC>(x.v[0]), from_f32<TC>(x.v[1]), from_f32<TC>(x.v[2]), from_f32<TC>(x.v[3]),
                   from_f32<TC>(x.v[4]), from_f32<TC>(x.v[5]), from_f32<TC>(x.v[6]), from_f32<TC>(x.v[7])};
-    store16_rs(r, elem * 2u, __builtin_bit_cast(u32x4, b));
+    store16_rs<AUX>(r, elem * 2u, __builtin_bit_cast(u32x4, b));
   } else {
-    store16_rs(r, elem * 4u, u32x4{__float_as_uint(x.v[0]), __float_as_uint(x.v[1]), __float_as_uint(x.v[2]),
+    store16_rs<AUX>(r, elem * 4u, u32x4{__float_as_uint(x.v[0]), __float_as_uint(x.v[1]), __float_as_uint(x.v[2]),
                                    __float_as_uint(x.v[3])});
-    store16_rs(r, elem * 4u + 16u, u32x4{__float_as_uint(x.v[4]), __float_as_uint(x.v[5]), __float_as_uint(x.v[6]),
+    store16_rs<AUX>(r, elem * 4u + 16u, u32x4{__float_as_uint(x.v[4]), __float_as_uint(x.v[5]), __float_as_uint(x.v[6]),
                                          __float_as_uint(x.v[7])});
   }
 }
@@ -314,7 +317,7 @@ F5H_DEV void store8_rs(__amdgpu_buffer_rsrc_t r, uint32_t elem, const V8& x) {
 // Per element the arithmetic is the same functions as before (bitwise identical results). The row data of
 // strip i+1 (RoPE pairs, residual chunks, row-mask bytes, addends) is fetched before strip i stores.
 // pre: PREF residual chunks prefetched before the K loop, [MT][NT/2].
-template <typename TC, int EPI, int MT, int NT, bool PREF, bool BIAS, int PM, int PT>
+template <typename TC, int EPI, int MT, int NT, bool PREF, bool BIAS, int PM, int PT, int AUX = 0>
 F5H_DEV void epilogue_direct_t(const GemmArgs& g, const f32x4 (&acc)[MT][NT], int rbase, int cbase, int lane,
                                const V8 (&pre)[PM][PT]) {
   static_assert(NT % 2 == 0, "column blocks in pairs");
@@ -458,7 +461,7 @@ F5H_DEV void epilogue_direct_t(const GemmArgs& g, const f32x4 (&acc)[MT][NT], in
           x.v[2 * p + 1] = rr.y;
         }
         (void)row;
-        store8_rs<TC>(dst, (uint32_t)(((ps_sq * g.heads + head) * g.seq_len + ps_pos) * 64 + dh[jp]), x);
+        store8_rs<TC, AUX>(dst, (uint32_t)(((ps_sq * g.heads + head) * g.seq_len + ps_pos) * 64 + dh[jp]), x);
       } else if constexpr (EPI == EPI_RESID || EPI == EPI_RESID16) {
         V8 c;
         if constexpr (PREF)
@@ -469,7 +472,7 @@ F5H_DEV void epilogue_direct_t(const GemmArgs& g, const f32x4 (&acc)[MT][NT], in
         V8 o;
 #pragma unroll
         for (int e = 0; e < 8; ++e) o.v[e] = resid_add(c.v[e], gate8[jp].v[e], x.v[e], keep);
-        store8_rs<ResT<TC, EPI>>(dst, (uint32_t)((int64_t)row * g.ldc + col), o);
+        store8_rs<ResT<TC, EPI>, AUX>(dst, (uint32_t)((int64_t)row * g.ldc + col), o);
       } else if constexpr (EPI == EPI_GELU_TANH || EPI == EPI_GELU_ERF_OP) {
         if constexpr (EPI == EPI_GELU_TANH && is16<TC>()) {
 #pragma unroll
@@ -482,9 +485,9 @@ F5H_DEV void epilogue_direct_t(const GemmArgs& g, const f32x4 (&acc)[MT][NT], in
 #pragma unroll
           for (int e = 0; e < 8; ++e) x.v[e] = EPI == EPI_GELU_ERF_OP ? gelu_erf(x.v[e]) : gelu_tanh(x.v[e]);
         }
-        store8_rs<TC>(dst, (uint32_t)((int64_t)row * g.ldc + col), x);
+        store8_rs<TC, AUX>(dst, (uint32_t)((int64_t)row * g.ldc + col), x);
       } else if constexpr (EPI == EPI_STORE16) {
-        store8_rs<TC>(dst, (uint32_t)((int64_t)row * g.ldc + col), x);
+        store8_rs<TC, AUX>(dst, (uint32_t)((int64_t)row * g.ldc + col), x);
       } else if constexpr (EPI == EPI_INPROJ) {
         // x.W_x^T + P for this branch's row, and for the other branch's row (same x, dit.py:162)
         V8 o0, o1;
@@ -498,23 +501,23 @@ F5H_DEV void epilogue_direct_t(const GemmArgs& g, const f32x4 (&acc)[MT][NT], in
         // rows >= M would land in the second block: drop them explicitly (an offset past the descriptor's
         // extent, which fast_epi_ok keeps below 0xF0000000 bytes; no 32-bit wrap for either 16-B half)
         constexpr uint32_t kPast = 0xF0000000u / 4;
-        store8_rs<float>(dst, row < g.M ? (uint32_t)((int64_t)row * g.ldc + col) : kPast, o0);
+        store8_rs<float, AUX>(dst, row < g.M ? (uint32_t)((int64_t)row * g.ldc + col) : kPast, o0);
         if (g.dual_rows)
-          store8_rs<float>(dst, row < g.M ? (uint32_t)((int64_t)(row + g.dual_rows) * g.ldc + col) : kPast, o1);
+          store8_rs<float, AUX>(dst, row < g.M ? (uint32_t)((int64_t)(row + g.dual_rows) * g.ldc + col) : kPast, o1);
       } else {  // EPI_STORE
-        store8_rs<float>(dst, (uint32_t)((int64_t)row * g.ldc + col), x);
+        store8_rs<float, AUX>(dst, (uint32_t)((int64_t)row * g.ldc + col), x);
       }
     }
     if constexpr (EPI == EPI_QKV) advance(ps_sq, ps_pos);
   });
 }
-template <typename TC, int EPI, int MT, int NT, bool PREF, int PM, int PT>
+template <typename TC, int EPI, int MT, int NT, bool PREF, int AUX = 0, int PM, int PT>
 F5H_DEV void epilogue_direct(const GemmArgs& g, const f32x4 (&acc)[MT][NT], int rbase, int cbase, int lane,
                              const V8 (&pre)[PM][PT]) {
   if (g.bias)
-    epilogue_direct_t<TC, EPI, MT, NT, PREF, true>(g, acc, rbase, cbase, lane, pre);
+    epilogue_direct_t<TC, EPI, MT, NT, PREF, true, PM, PT, AUX>(g, acc, rbase, cbase, lane, pre);
   else
-    epilogue_direct_t<TC, EPI, MT, NT, PREF, false>(g, acc, rbase, cbase, lane, pre);
+    epilogue_direct_t<TC, EPI, MT, NT, PREF, false, PM, PT, AUX>(g, acc, rbase, cbase, lane, pre);
 }
 
 
@@ -525,8 +528,13 @@ F5H_DEV void epilogue_direct(const GemmArgs& g, const f32x4 (&acc)[MT][NT], int 
 // + 144 AGPR = 260: one block per CU, so the C2 QKV GEMM (480 tiles) ran as two rounds on 256 CUs
 // (tools/timeline_c2.py: second half of the grid entering 24 us after the first). Declaring 2 waves
 // per SIMD it fits in 212 VGPR, no spill.
-template <typename TC, int EPI, int BM, int BN, int WGM, int WGN, int NS, bool FAST = false, int KB = 128>
-__global__ __launch_bounds__(64 * WGM * WGN, 2) void gemm_kernel(GemmArgs g) {
+// The block body of gemm_kernel: block b of nwg (XCD-remapped below) computes one BM x BN tile in the LDS
+// image `lds`. PUB (the in-launch phase chain, chain.hip): stores are write-through and the tile's row groups are
+// published to dep.pub; a non-null dep.wait makes the block wait for its row groups' producers before its
+// first operand load; blocks past the last tile (the chain pads each phase to whole XCD rounds) do nothing.
+template <typename TC, int EPI, int BM, int BN, int WGM, int WGN, int NS, bool FAST, int KB, bool PUB = false,
+          bool CHAIN = false>
+F5H_DEV void gemm_body(const GemmArgs& g, const int b, const int nwg, uint4* lds, const ChainDep& dep) {
   const ProbeT probe_t = probe_enter(g.probe);
   typedef GemmCfg<BM, BN, WGM, WGN, NS, KB> C;
   constexpr int E = elems16<TC>();
@@ -539,18 +547,21 @@ __global__ __launch_bounds__(64 * WGM * WGN, 2) void gemm_kernel(GemmArgs g) {
   typedef typename Slab<TC>::frag frag;
   auto swz = [](int row, int chunk) { return KB == 128 ? swz128g(row, chunk) : swz64(row, chunk); };
 
-  __shared__ __attribute__((aligned(16))) uint4 lds[C::bytes / 16];
   constexpr int stage_u4 = C::stage_bytes / 16;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid / WGN, wn = wid % WGN;
   const int ntn = (g.N + BN - 1) / BN;
   // XCD-aware remap (cdna_hip_programming.md T1, bijective form): blocks b and b+8 share an
   // XCD, so give each XCD a contiguous run of n-fastest tiles -> its L2 holds whole A panels
-  const int nwg = gridDim.x, b = blockIdx.x, xq = nwg >> 3, xr = nwg & 7, xcd = b & 7;
+  const int xq = nwg >> 3, xr = nwg & 7, xcd = b & 7;
   const int bid = (xcd < xr ? xcd * (xq + 1) : xr * (xq + 1) + (xcd - xr) * xq) + (b >> 3);
+  if constexpr (CHAIN) {
+    if (bid >= ((g.M + BM - 1) / BM) * ntn) return;
+  }
   // with the pad skip, row tiles of padding cluster by sequence: spread the m-rows over the XCDs
   const int mrow = g.live_len ? spread8(bid / ntn, (g.M + BM - 1) / BM) : bid / ntn;
   const int m0 = mrow * BM, n0 = (bid % ntn) * BN;
+  if constexpr (CHAIN) chain_wait(dep, g.M, m0, BM);
   if constexpr (EPI == EPI_RESID || EPI == EPI_RESID16) {
     if (!tile_live(g, m0, BM)) {  // every row padding: nothing to add (C2's B = 1 never passes live_len)
       probe_exit(g.probe, probe_t);
@@ -739,8 +750,10 @@ __global__ __launch_bounds__(64 * WGM * WGN, 2) void gemm_kernel(GemmArgs g) {
   // the strip loop covers an older store (one strip of global round trips instead of one per
   // chunk; measured 9.5 us of a 30.6 us QKV launch before).
   constexpr bool FAST_EPI = FAST && NT % 2 == 0;
+  static_assert(FAST_EPI || !PUB, "the chain publishes from the direct epilogue");
   if constexpr (FAST_EPI) {
-    epilogue_direct<TC, EPI, MT, NT, PREF>(g, acc, m0 + wm * WM, n0 + wn * WN, lane, pre);
+    epilogue_direct<TC, EPI, MT, NT, PREF, PUB ? kAuxWT : 0>(g, acc, m0 + wm * WM, n0 + wn * WN, lane, pre);
+    if constexpr (PUB) chain_publish(dep, g.M, m0, BM);
   }
   if constexpr (!FAST_EPI) {
 #pragma unroll
@@ -766,6 +779,12 @@ __global__ __launch_bounds__(64 * WGM * WGN, 2) void gemm_kernel(GemmArgs g) {
     }
   }
   probe_exit(g.probe, probe_t);
+}
+
+template <typename TC, int EPI, int BM, int BN, int WGM, int WGN, int NS, bool FAST = false, int KB = 128>
+__global__ __launch_bounds__(64 * WGM * WGN, 2) void gemm_kernel(GemmArgs g) {
+  __shared__ __attribute__((aligned(16))) uint4 lds[GemmCfg<BM, BN, WGM, WGN, NS, KB>::bytes / 16];
+  gemm_body<TC, EPI, BM, BN, WGM, WGN, NS, FAST, KB>(g, blockIdx.x, gridDim.x, lds, ChainDep{});
 }
 
 // ======================================================================================

@@ -220,4 +220,39 @@ struct PackArgs {
 };
 hipError_t pack_strided(const PackArgs& a, hipStream_t st);
 
+// ---- In-launch phase chain (chain.hip): the row-local seams of a DiT block-step (out-proj -> LayerNorm ->
+// FFN1 -> FFN2 -> LayerNorm -> next QKV) as ONE launch whose phases hand row groups (kChainRows rows) to the
+// next phase through per-group arrival counters (cdna_hip_programming.md §6 Guideline 16, R1: write-through
+// payload, drained, one counter add per workgroup; the consumer polls relaxed and acquires once).
+constexpr int kChainRows = 64;
+struct ChainDep {
+  const unsigned* wait;  // the producer phase's row-group counters (null: no in-launch producer)
+  int wait_mult, wait_unit;  // a complete group holds wait_mult * ceil(rows of the group / wait_unit) arrivals
+  unsigned* pub;         // this phase's row-group counters (null: last phase)
+  unsigned* err;         // set to 1 when a wait gives up (bounded spin); the results are then garbage
+};
+struct LnArgs {
+  const void* h;  // [M, 1024] residual stream (operand dtype)
+  void* out;      // [M, 1024] LN(h) * (1 + scale) + shift
+  const float* shift;
+  const float* scale;
+};
+struct ChainArgs {
+  GemmArgs out, ff1, ff2, qkv;  // qkv.M == 0: no QKV phase (the model's last layer)
+  LnArgs ln1, ln2;
+  unsigned* cnt;   // [5][groups] arrival counters, zero before the launch
+  int groups;      // ceil(M / kChainRows) (stride of cnt)
+};
+// bytes of cnt a chain launch over M rows uses (the caller zeroes them before every launch)
+inline size_t chain_counter_bytes(int M) {
+  return (size_t)5 * ((M + kChainRows - 1) / kChainRows) * sizeof(unsigned);
+}
+// Launch the chain (16-bit operands, dim 1024, whole-column tiles); hipErrorInvalidValue when the shapes do not
+// fit it (the caller then issues the separate launches).
+hipError_t chain_launch(int compute, const ChainArgs& a, hipStream_t st);
+// the give-up word of the chain's bounded waits: returns it and clears it (host call, synchronous)
+int chain_fault_take();
+// chain launches enqueued by this process
+int64_t chain_launches();
+
 }  // namespace f5h

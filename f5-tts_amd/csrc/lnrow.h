@@ -82,4 +82,44 @@ F5H_DEV void ln_mod_row(const float4 (&v)[V], const float4 (&a)[V], const float4
   }
 }
 
+// The 16-bit residual stream at d = 1024 (ln_mod16_kernel, and the chain's LayerNorm phase, chain.hip): lane l
+// holds elements 8(l + 64k) .. +7 (k < 2) of the row in x[k] (raw 16-byte chunks), a/b the scale/shift of
+// those elements; o[k] the normalised, modulated chunks. One function, so both launches give the same bits.
+template <typename T>
+F5H_DEV void ln16_row(const uint4 (&x)[2], const float4 (&a)[2][2], const float4 (&b)[2][2], uint4 (&o)[2]) {
+  typedef typename Op16<T>::v8 v8;
+  constexpr int d = 1024;
+  float v[2][8];
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const v8 w = __builtin_bit_cast(v8, x[k]);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[k][e] = to_f32(w[e]);
+  }
+  float s = 0.f;
+#pragma unroll
+  for (int k = 0; k < 2; ++k)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) s += v[k][e];
+  const float mean = wave_sum_dpp(s) / d;
+  float q = 0.f;
+#pragma unroll
+  for (int k = 0; k < 2; ++k)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const float p = v[k][e] - mean;
+      q += p * p;
+    }
+  const float rstd = rsqrtf(wave_sum_dpp(q) / d + 1e-6f);
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const float av[8] = {a[k][0].x, a[k][0].y, a[k][0].z, a[k][0].w, a[k][1].x, a[k][1].y, a[k][1].z, a[k][1].w};
+    const float bv[8] = {b[k][0].x, b[k][0].y, b[k][0].z, b[k][0].w, b[k][1].x, b[k][1].y, b[k][1].z, b[k][1].w};
+    v8 w;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) w[e] = from_f32<T>((v[k][e] - mean) * rstd * (1.f + av[e]) + bv[e]);
+    o[k] = __builtin_bit_cast(uint4, w);
+  }
+}
+
 }  // namespace f5h

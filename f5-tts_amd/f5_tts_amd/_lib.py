@@ -39,6 +39,8 @@ EXPORTS = (
     "f5h_set_cfg_streams",
     "f5h_graph_stats",
     "f5h_set_pad_skip",
+    "f5h_set_chain",
+    "f5h_chain_stats",
     "f5h_op_linear",
     "f5h_op_attention",
     "f5h_gemm_force_config",
@@ -161,6 +163,11 @@ def lib():
     if hasattr(L, "f5h_attn_force_safe"):
         L.f5h_attn_force_safe.argtypes = [i32]
         L.f5h_attn_force_safe.restype = ctypes.c_int
+    if hasattr(L, "f5h_set_chain"):
+        L.f5h_set_chain.argtypes = [vp, i32]
+        L.f5h_set_chain.restype = ctypes.c_int
+        L.f5h_chain_stats.argtypes = [ctypes.POINTER(i64), ctypes.POINTER(i32)]
+        L.f5h_chain_stats.restype = ctypes.c_int
     if hasattr(L, "f5h_debug_tile_live"):
         L.f5h_debug_tile_live.argtypes = [vp, i32, i32, i32, i32]
         L.f5h_debug_tile_live.restype = ctypes.c_int

@@ -126,6 +126,11 @@ class Engine:
         padding only; default on). Results are bitwise identical either way."""
         _lib.check(_lib.lib().f5h_set_pad_skip(self._h, int(bool(on))), "set_pad_skip")
 
+    def set_chain(self, on: bool):
+        """Run each DiT layer's row-local seams (out-proj .. next QKV) as one phase-chain launch (16-bit DiT
+        path without row masks; f5h_set_chain). Results are bitwise identical either way."""
+        _lib.check(_lib.lib().f5h_set_chain(self._h, int(bool(on))), "set_chain")
+
     def graph_stats(self):
         cap, rep, n = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int32()
         _lib.check(_lib.lib().f5h_graph_stats(self._h, ctypes.byref(cap), ctypes.byref(rep), ctypes.byref(n)),
@@ -282,3 +287,11 @@ def attn_force_safe(on: bool):
 def gemm_force_config(cfg: int = -1):
     """Pin the 16-bit GEMM tile configuration (0, 1, 5, 11) for this process; -1 = automatic."""
     _lib.check(_lib.lib().f5h_gemm_force_config(int(cfg)), "gemm_force_config")
+
+
+def chain_stats():
+    """Test hook: (phase-chain launches enqueued by this process, 1 if one gave up waiting for a producer since
+    the last call, else 0; cleared)."""
+    n, f = ctypes.c_int64(), ctypes.c_int32()
+    _lib.check(_lib.lib().f5h_chain_stats(ctypes.byref(n), ctypes.byref(f)), "chain_stats")
+    return int(n.value), int(f.value)

@@ -213,6 +213,15 @@ int f5h_graph_stats(f5h_engine* eng, int64_t* captures, int64_t* replays, int32_
  * tiles of padding only skip their work (the rows keep their residual, as masked rows of a computed tile
  * do). 1 (default; env F5H_NO_PAD_SKIP=1 at creation: 0) or 0 to compute every block. Bitwise identical. */
 int f5h_set_pad_skip(f5h_engine* eng, int32_t enable);
+/* 16-bit DiT path without row masks: run each layer's out-proj, LayerNorm, FFN1, FFN2 and the next layer's
+ * LayerNorm + QKV (modules.py:743-757) as ONE launch whose phases hand 64-row groups to each other through
+ * arrival counters (chain.hip, DESIGN.md §3 'Phase chain'), instead of six launches. 1 or 0 (default; env
+ * F5H_CHAIN=1 at creation: 1). Bitwise identical results. */
+int f5h_set_chain(f5h_engine* eng, int32_t enable);
+/* Test hook: *launches = phase-chain launches this process has enqueued (eager launches and graph captures);
+ * *fault = 1 if one of them gave up waiting for a producer (a bounded wait that should never expire; its
+ * results are then wrong), else 0; the flag is cleared. Synchronous. Either pointer may be NULL. */
+int f5h_chain_stats(int64_t* launches, int32_t* fault);
 
 /* Op-level entry points (parity tests / microbenchmarks). Device pointers, row-major. */
 /* C[M,N] = A[M,K] . W[N,K]^T + bias  (fp32 in/out; compute = F5H_FP32 or F5H_BF16 operands) */

@@ -575,3 +575,52 @@ def test_cfg_branch_chains_bitwise_equal(compute):
     for mode in ("two", "eager"):
         assert torch.equal(outs[mode][0], outs["one"][0]), mode
         assert torch.equal(outs[mode][1], outs["one"][1]), mode
+
+
+@pytest.mark.parametrize("compute", ["bf16", "fp16"])
+def test_phase_chain_bitwise_equal(compute):
+    """The in-launch phase chain (f5h_set_chain: out-proj .. FFN2 + the next layer's LayerNorm and QKV as one
+    launch, 64-row groups handed over by arrival counters, chain.hip) gives bitwise the result of the separate
+    launches: single-utterance calls at ragged row counts (M not a multiple of 64 or 192), in graph mode and
+    eager, with the packed CFG chain and with the two CFG parts on their own streams (their own counters). Every
+    launch of the chained run must have been a chain launch (the launch counter moves by the layer count per
+    step) and no wait may have given up."""
+    _need_gpu()
+    from f5_tts_amd.engine import chain_stats
+
+    arch = configs.get_arch("F5TTS_v1_Base", depth=3)
+    m = _model(arch, compute)
+    eng = m.transformer.get_engine(compute, m.device)
+    chain_stats()  # clear the fault flag
+    try:
+        for ref, total, nt in ((37, 149, 20), (250, 611, 60)):
+            inp = synthetic.make_case(B=1, ref_frames=[ref], total_frames=[total], n_text=[nt],
+                                      vocab=arch["text_num_embeds"])
+            dur = torch.maximum(torch.maximum((inp["text"] != -1).sum(-1), inp["lens"]) + 1, inp["duration"])
+            y0 = synthetic.reference_noise(dur, 3).to(DEV)
+            kw = dict(cond=inp["cond"].to(DEV), text=inp["text"].to(DEV), duration=inp["duration"], lens=inp["lens"],
+                      steps=4, cfg_strength=2.0, sway_sampling_coef=-1.0, y0=y0)
+            outs = {}
+            for mode in ("plain", "chain", "chain_eager", "chain_two"):
+                eng.set_chain(mode != "plain")
+                eng.set_graph_mode(mode != "chain_eager")
+                eng.set_cfg_streams(2 if mode == "chain_two" else 1)
+                n0, _ = chain_stats()
+                out, traj = m.sample(**kw)
+                torch.cuda.synchronize()
+                n1, fault = chain_stats()
+                assert fault == 0, (total, mode)
+                if mode == "chain_eager":
+                    assert n1 - n0 == 4 * arch["depth"], (total, mode, n1 - n0)  # every layer of every step
+                elif mode != "plain":
+                    assert n1 - n0 in (0, arch["depth"], 2 * arch["depth"]), (total, mode, n1 - n0)  # captures
+                else:
+                    assert n1 == n0
+                outs[mode] = (out.clone(), traj.clone())
+            for mode in ("chain", "chain_eager", "chain_two"):
+                assert torch.equal(outs[mode][0], outs["plain"][0]), (total, mode)
+                assert torch.equal(outs[mode][1], outs["plain"][1]), (total, mode)
+    finally:
+        eng.set_chain(False)
+        eng.set_graph_mode(True)
+        eng.set_cfg_streams(0)
