@@ -561,7 +561,6 @@ F5H_DEV void gemm_body(const GemmArgs& g, const int b, const int nwg, uint4* lds
   // with the pad skip, row tiles of padding cluster by sequence: spread the m-rows over the XCDs
   const int mrow = g.live_len ? spread8(bid / ntn, (g.M + BM - 1) / BM) : bid / ntn;
   const int m0 = mrow * BM, n0 = (bid % ntn) * BN;
-  if constexpr (CHAIN) chain_wait(dep, g.M, m0, BM);
   if constexpr (EPI == EPI_RESID || EPI == EPI_RESID16) {
     if (!tile_live(g, m0, BM)) {  // every row padding: nothing to add (C2's B = 1 never passes live_len)
       probe_exit(g.probe, probe_t);
@@ -596,9 +595,8 @@ F5H_DEV void gemm_body(const GemmArgs& g, const int b, const int nwg, uint4* lds
   const TC* A2 = reinterpret_cast<const TC*>(g.A2);
   const __amdgpu_buffer_rsrc_t wrs =
       rsrc_of(W + (int64_t)n0 * g.ldw, wbytes);
-  auto stage = [&](int buf, int k0) {
+  auto stage_a = [&](int buf, int k0) {
     uint4* As = lds + buf * stage_u4;
-    uint4* Bs = As + BM * CPR;
     const bool second = A2 && k0 >= g.k_split;
     const TC* Ab = second ? A2 : A;
     const int ka = second ? k0 - g.k_split : k0;
@@ -608,10 +606,17 @@ F5H_DEV void gemm_body(const GemmArgs& g, const int b, const int nwg, uint4* lds
       constexpr int i = decltype(I)::value;
       dma16(ars, (LDS_PTR(void))(As + (i * NW + wid_s) * 64), aoff[i], ka * ESZ);
     });
+  };
+  auto stage_w = [&](int buf, int k0) {
+    uint4* Bs = lds + buf * stage_u4 + BM * CPR;
     static_for<0, BR>([&](auto I) {
       constexpr int i = decltype(I)::value;
       dma16(wrs, (LDS_PTR(void))(Bs + (i * NW + wid_s) * 64), boff[i], k0 * ESZ);
     });
+  };
+  auto stage = [&](int buf, int k0) {
+    stage_a(buf, k0);
+    stage_w(buf, k0);
   };
 
   // Fragment reads are inline-asm ds_read_b128 so that hipcc does not put a vmcnt(0) (for the
@@ -636,7 +641,16 @@ F5H_DEV void gemm_body(const GemmArgs& g, const int b, const int nwg, uint4* lds
     for (int j = 0; j < NT; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   const int nk = g.K / BKE;
-  for (int p = 0; p < NS - 1 && p < nk; ++p) stage(p, p * BKE);
+  if constexpr (CHAIN) {
+    // phase chain: the weight panels of the first stages (no producer in the launch) are in flight while the
+    // block waits for its rows; the activation panels follow the acquire. Issue order W0 .. W(NS-2), A0 ..
+    // A(NS-2): the first wait below counts activation pieces only.
+    for (int p = 0; p < NS - 1 && p < nk; ++p) stage_w(p, p * BKE);
+    chain_wait(dep, g.M, m0, BM);
+    for (int p = 0; p < NS - 1 && p < nk; ++p) stage_a(p, p * BKE);
+  } else {
+    for (int p = 0; p < NS - 1 && p < nk; ++p) stage(p, p * BKE);
+  }
   asm volatile("" ::: "memory");  // the residual loads below stay behind the stage DMA
   // EPI_RESID: the residual rows this lane's epilogue reads are fetched right behind the first
   // operand stages (so they do not delay stage 0: the first wait leaves them in flight, the second
@@ -668,10 +682,14 @@ F5H_DEV void gemm_body(const GemmArgs& g, const int b, const int nwg, uint4* lds
   for (int kt = 0; kt < nk; ++kt) {
     // stage kt has landed for THIS wave once at most the younger in-flight stages remain;
     // the barrier then publishes every wave's part of it
-    if (kt == 0)
-      wait_stages<DPS, NPRE>(min(NS - 2, nk - 1));
-    else
+    if (kt == 0) {
+      if constexpr (CHAIN)
+        wait_stages<AR, NPRE>(min(NS - 2, nk - 1));  // younger than A0: A1 .. A(NS-2) and the residual loads
+      else
+        wait_stages<DPS, NPRE>(min(NS - 2, nk - 1));
+    } else {
       wait_stages<DPS>(min(NS - 2, nk - 1 - kt));
+    }
     __builtin_amdgcn_s_barrier();
     if (kt == 0) probe_mark(g.probe, probe_t, 1);
     const uint32_t soff = (uint32_t)((kt % NS) * C::stage_bytes);
