@@ -511,6 +511,96 @@ F5H_DEV void epilogue_direct_t(const GemmArgs& g, const f32x4 (&acc)[MT][NT], in
     if constexpr (EPI == EPI_QKV) advance(ps_sq, ps_pos);
   });
 }
+// QKV epilogue through the wave's LDS strip (gemm_kernel): per 16-row strip the accumulators go to LDS (one
+// ds_write_b128 per block: the swapped-operand layout already holds four consecutive columns per lane) and come
+// back by rows, 8 lanes per 64-column head row, so every store instruction writes 8 whole 128-B rows of q/k/v.
+// The direct epilogue's stores cover 16 rows x 64 B each (two instructions per row): measured 28.4 against
+// 26.0 us per C2 QKV launch (profiles/r05_ab_c2_attention_epilogue.txt). Same per-element arithmetic as the
+// direct form (bitwise identical).
+template <typename TC, int MT, int NT, int EPAD, bool BIAS>
+F5H_DEV void epilogue_qkv_strip_t(const GemmArgs& g, const f32x4 (&acc)[MT][NT], float* Cs, int rbase, int cbase,
+                                  int lane) {
+  constexpr int WN = NT * 16, CH = WN / 8, TPC = 16 * CH / 64;
+  static_assert(WN == 64, "a wave's 64 columns are one head");
+  const int fr = lane & 15, q = lane >> 4;
+  const int cc = lane % CH, col = cbase + cc * 8;
+  V8 bias8 = V8{};
+  if constexpr (BIAS) bias8 = load8(g.bias + col);
+  const int inner = g.heads * 64;
+  const int which = __builtin_amdgcn_readfirstlane(fdiv(cbase, inner));
+  const int head = __builtin_amdgcn_readfirstlane((cbase - which * inner) >> 6);
+  const int dh = (col - which * inner) & 63;
+  const bool rope_on = which < 2 && head < g.rope_heads;
+  const float qsc = (which == 0 && g.q_scale != 0.f) ? g.q_scale : 1.f;
+  const __amdgpu_buffer_rsrc_t dst =
+      rsrc_of(which == 0 ? g.q : (which == 1 ? g.k : g.v), (uint64_t)g.M * inner * sizeof(TC));
+  int pf_sq[TPC], pf_pos[TPC], ps_sq[TPC], ps_pos[TPC];
+#pragma unroll
+  for (int t = 0; t < TPC; ++t) {
+    const int row0 = rbase + t * (64 / CH) + lane / CH;
+    pf_sq[t] = ps_sq[t] = fdiv(row0, g.seq_len);
+    pf_pos[t] = ps_pos[t] = row0 - pf_sq[t] * g.seq_len;
+  }
+  auto advance = [&](int& sq, int& pos) {
+    pos += 16;
+    while (pos >= g.seq_len) {
+      pos -= g.seq_len;
+      ++sq;
+    }
+  };
+  u32x4 rp[2][TPC][2];  // RoPE (cos, sin) of the chunk's four pairs, fetched one strip ahead
+  auto fetch = [&](u32x4 (&r)[TPC][2]) {
+#pragma unroll
+    for (int t = 0; t < TPC; ++t) {
+      const u32x4* p = reinterpret_cast<const u32x4*>(g.rope + pf_pos[t] * 32 + (dh >> 1));
+      r[t][0] = p[0];
+      r[t][1] = p[1];
+      advance(pf_sq[t], pf_pos[t]);
+    }
+  };
+  fetch(rp[0]);
+  static_for<0, MT>([&](auto I) {
+    constexpr int i = decltype(I)::value;
+    if constexpr (i + 1 < MT) fetch(rp[(i + 1) & 1]);
+#pragma unroll
+    for (int j = 0; j < NT; ++j) *reinterpret_cast<f32x4*>(Cs + fr * EPAD + j * 16 + 4 * q) = acc[i][j];
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+    for (int t = 0; t < TPC; ++t) {
+      const int rr = t * (64 / CH) + lane / CH;
+      const float* src = Cs + rr * EPAD + cc * 8;
+      const float4 a0 = *reinterpret_cast<const float4*>(src), a1 = *reinterpret_cast<const float4*>(src + 4);
+      V8 x{{a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w}};
+      if constexpr (BIAS) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) x.v[e] = add_nc(x.v[e], bias8.v[e]);
+      }
+      const u32x4* cs4 = rp[i & 1][t];
+#pragma unroll
+      for (int p = 0; p < 4; ++p) {
+        const float c = __uint_as_float(cs4[p >> 1][2 * (p & 1)]), sn = __uint_as_float(cs4[p >> 1][2 * (p & 1) + 1]);
+        const f32x2 ab = {x.v[2 * p], x.v[2 * p + 1]};
+        f32x2 r;
+        {
+#pragma clang fp contract(off)
+          const f32x2 pc = ab * c, ps = f32x2{ab.y, ab.x} * sn;
+          r = pc + f32x2{-ps.x, ps.y};
+          r = (rope_on ? r : ab) * qsc;  // exact for qsc = 1 (k, v columns)
+        }
+        x.v[2 * p] = r.x;
+        x.v[2 * p + 1] = r.y;
+      }
+      store8_rs<TC>(dst, (uint32_t)(((ps_sq[t] * g.heads + head) * g.seq_len + ps_pos[t]) * 64 + dh), x);
+      advance(ps_sq[t], ps_pos[t]);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  });
+}
+
 template <typename TC, int EPI, int MT, int NT, bool PREF, int AUX = 0, int PM, int PT>
 F5H_DEV void epilogue_direct(const GemmArgs& g, const f32x4 (&acc)[MT][NT], int rbase, int cbase, int lane,
                              const V8 (&pre)[PM][PT]) {
@@ -769,7 +859,13 @@ F5H_DEV void gemm_body(const GemmArgs& g, const int b, const int nwg, uint4* lds
   // chunk; measured 9.5 us of a 30.6 us QKV launch before).
   constexpr bool FAST_EPI = FAST && NT % 2 == 0;
   static_assert(FAST_EPI || !PUB, "the chain publishes from the direct epilogue");
-  if constexpr (FAST_EPI) {
+  if constexpr (FAST_EPI && EPI == EPI_QKV && !PUB) {
+    float* Cq = reinterpret_cast<float*>(lds) + wid * 16 * C::EPAD;
+    if (g.bias)
+      epilogue_qkv_strip_t<TC, MT, NT, C::EPAD, true>(g, acc, Cq, m0 + wm * WM, n0 + wn * WN, lane);
+    else
+      epilogue_qkv_strip_t<TC, MT, NT, C::EPAD, false>(g, acc, Cq, m0 + wm * WM, n0 + wn * WN, lane);
+  } else if constexpr (FAST_EPI) {
     epilogue_direct<TC, EPI, MT, NT, PREF, PUB ? kAuxWT : 0>(g, acc, m0 + wm * WM, n0 + wn * WN, lane, pre);
     if constexpr (PUB) chain_publish(dep, g.M, m0, BM);
   }
