@@ -1632,8 +1632,8 @@ int f5h_op_linear(void* stream, int32_t compute, int32_t M, int32_t N, int32_t K
 }
 
 int f5h_gemm_force_config(int32_t cfg) {
-  if (cfg != -1 && cfg != 0 && cfg != 1 && cfg != 5 && cfg != 11 && cfg != 12 && cfg != 13)
-    return fail(F5H_EINVAL, "gemm config must be -1, 0, 1, 5, 11, 12 or 13");
+  if (cfg != -1 && cfg != 0 && cfg != 1 && cfg != 5 && (cfg < 11 || cfg > 16))
+    return fail(F5H_EINVAL, "gemm config must be -1, 0, 1, 5 or 11-16");
   gemm_force_config(cfg);
   g_kernel_epoch.fetch_add(1);
   return 0;

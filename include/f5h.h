@@ -235,7 +235,7 @@ int f5h_op_attention(void* stream, int32_t compute, int32_t S, int32_t H, int32_
                      void* workspace, size_t workspace_bytes);
 
 /* Tuning/test hook: pin the 16-bit GEMM tile configuration for all later launches in this
- * process (0, 1, 5, 11, 12, 13), or -1 to restore the automatic per-shape choice. */
+ * process (0, 1, 5, 11-16; 14-16 only for the QKV, residual and GELU epilogues), or -1 to restore the automatic per-shape choice. */
 int f5h_gemm_force_config(int32_t cfg);
 /* Test hook: on != 0 makes every later 16-bit attention launch of this process rerun each workgroup's key
  * loop in its lazy-running-max form (the path a row takes when a score runs far above its first tile's max;
