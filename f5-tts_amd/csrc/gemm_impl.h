@@ -306,7 +306,229 @@ F5H_DEV void store8_rs(__amdgpu_buffer_rsrc_t r, uint32_t elem, const V8& x) {
   }
 }
 
-// Direct epilogue (round 5): the MFMAs run with swapped operands (W fragment as A, activation fragment as B),
+// Fast epilogue of one wave's sub-tile (whole-column tiles of the hot epilogues), per 16-row strip:
+// accumulators -> the wave's LDS strip (fp32, EPAD-float rows; one ds_write_b128 per block, the swapped-operand
+// layout holding four consecutive columns per lane) -> 8-column chunks of whole rows, so that every store
+// instruction writes whole 128-B row segments (the register-only epilogue below stores 64-B row pieces, two
+// instructions per segment: QKV +10-13 % and the residual GEMMs +5-8 % per launch at C4/C5, QKV +9 % at C2,
+// profiles/r05_ab_c4_c5_epilogue.txt). A lane's
+// column chunk is the same in every strip, so bias/gate/QKV head indices are loaded once, and the row
+// data of strip i+1 (RoPE pairs, residual rows, row-mask bytes) is fetched before strip i stores.
+// The strip loop has no control flow: bias presence is a template choice, per-lane choices (RoPE on
+// this column, rows past M) are selects or the store descriptor's range check. Any branch or any
+// arithmetic on a just-loaded value makes hipcc wait for that load, and on gfx9 every store issued
+// before it counts in the same vmcnt: at C3 such waits made the 256x256 ping-pong epilogue 13-15 us per
+// tile (profiles/r03_timeline_c3.txt). rbase/cbase: the sub-tile's first row/column.
+// Shared by gemm_kernel and gemm_pp_kernel.
+template <typename TC, int EPI, int MT, int NT, int WN, int EPAD, bool PREF, bool BIAS, int PM, int PT, int AUX = 0>
+F5H_DEV void epilogue_fast_t(const GemmArgs& g, const f32x4 (&acc)[MT][NT], float* Cs, int rbase, int cbase,
+                             int lane, const V8 (&pre)[PM][PT]) {
+  constexpr int CH = WN / 8;          // 8-column chunks per strip row
+  constexpr int TPC = 16 * CH / 64;   // chunks per lane per strip
+  static_assert(64 % CH == 0 && (16 * CH) % 64 == 0, "whole chunks per lane");
+  const int fr = lane & 15, q = lane >> 4;
+  const int cc = lane % CH;
+  const int col = cbase + cc * 8;
+  V8 bias8 = V8{};
+  if constexpr (BIAS) bias8 = load8(g.bias + col);
+  V8 gate8 = V8{{1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f}};
+  if constexpr (EPI == EPI_RESID || EPI == EPI_RESID16)
+    if (g.gate) gate8 = load8(g.gate + col);
+  int which = 0, head = 0, dh = 0;
+  bool rope_on = false;
+  float qsc = 1.f;
+  __amdgpu_buffer_rsrc_t dst;
+  if constexpr (EPI == EPI_QKV) {
+    // a wave's 64 columns are one head of one of q/k/v (cbase % 64 == 0): wave-uniform, so the
+    // destination descriptor lives in scalar registers (a per-lane one costs a waterfall loop per store)
+    static_assert(WN <= 64 && 64 % WN == 0, "a wave's columns lie in one head");
+    const int inner = g.heads * 64;
+    which = __builtin_amdgcn_readfirstlane(fdiv(cbase, inner));
+    const int hc = col - which * inner;
+    head = hc >> 6;
+    dh = hc & 63;
+    rope_on = which < 2 && head < g.rope_heads;
+    qsc = (which == 0 && g.q_scale != 0.f) ? g.q_scale : 1.f;
+    dst = rsrc_of(which == 0 ? g.q : (which == 1 ? g.k : g.v), (uint64_t)g.M * inner * sizeof(TC));
+  } else {
+    constexpr int OES = (EPI == EPI_STORE || EPI == EPI_RESID || EPI == EPI_INPROJ) ? 4 : (int)sizeof(TC);
+    dst = rsrc_of(g.C, (uint64_t)(g.M + (EPI == EPI_INPROJ ? g.dual_rows : 0)) * g.ldc * OES);
+  }
+  // Loads only, raw bits, no arithmetic on their results here (see above): conversions happen at the
+  // use, one strip later. Row indices are clamped instead of branched on (rows >= M are never stored).
+  struct RowIn {
+    u32x4 d0, d1;  // RoPE (cos, sin) of four pairs (QKV, fp32), the residual row chunk (RESID), the addend (INPROJ)
+    u32x4 e0, e1;  // INPROJ: the second output row's addend
+    uint32_t kb;   // RESID row-mask byte
+  };
+  const __amdgpu_buffer_rsrc_t rk = rsrc_of(g.rowkeep, g.rowkeep ? (uint64_t)g.M : 0);  // null: reads 0
+  const bool masked = g.rowkeep != nullptr;
+  // QKV: (sequence, position) of each of the lane's chunk rows, for the strip being fetched (pf) and the one being
+  // stored (ps), advanced by 16 rows per strip (one division per chunk row for the whole epilogue, not two per
+  // strip). Rows past M get positions too: the RoPE table index stays in range and their stores are dropped.
+  int pf_sq[TPC], pf_pos[TPC], ps_sq[TPC], ps_pos[TPC];
+  if constexpr (EPI == EPI_QKV) {
+#pragma unroll
+    for (int t = 0; t < TPC; ++t) {
+      const int row0 = rbase + t * (64 / CH) + lane / CH;
+      pf_sq[t] = ps_sq[t] = fdiv(row0, g.seq_len);
+      pf_pos[t] = ps_pos[t] = row0 - pf_sq[t] * g.seq_len;
+    }
+  }
+  auto advance = [&](int& sq, int& pos) {
+    pos += 16;
+    while (pos >= g.seq_len) {
+      pos -= g.seq_len;
+      ++sq;
+    }
+  };
+  auto fetch = [&](int i, RowIn (&ri)[TPC]) {
+#pragma unroll
+    for (int t = 0; t < TPC; ++t) {
+      const int rr = t * (64 / CH) + lane / CH;
+      const int rowc = min(rbase + i * 16 + rr, g.M - 1);
+      if constexpr (EPI == EPI_QKV) {
+        (void)rowc;
+        const u32x4* p = reinterpret_cast<const u32x4*>(g.rope + pf_pos[t] * 32 + (dh >> 1));
+        ri[t].d0 = p[0];
+        ri[t].d1 = p[1];
+        advance(pf_sq[t], pf_pos[t]);
+      } else if constexpr (EPI == EPI_RESID || EPI == EPI_RESID16) {
+        if constexpr (!PREF) {
+          const u32x4* p = reinterpret_cast<const u32x4*>(reinterpret_cast<const ResT<TC, EPI>*>(
+                                                              g.resid ? g.resid : g.C) + (int64_t)rowc * g.ldc + col);
+          ri[t].d0 = p[0];
+          if constexpr (sizeof(ResT<TC, EPI>) == 4) ri[t].d1 = p[1];  // fp32 rows: 32 B
+        }
+        ri[t].kb = __builtin_amdgcn_raw_buffer_load_b8(rk, (uint32_t)rowc, 0, 0);
+      } else if constexpr (EPI == EPI_INPROJ) {
+        const u32x4* p = reinterpret_cast<const u32x4*>(g.add + (int64_t)rowc * g.ld_add + col);
+        ri[t].d0 = p[0];
+        ri[t].d1 = p[1];
+        const u32x4* p2 = reinterpret_cast<const u32x4*>(g.add + (int64_t)(rowc + g.dual_rows) * g.ld_add + col);
+        ri[t].e0 = p2[0];  // (rows [M, M + dual_rows) of the addend; the first rows again when dual_rows = 0)
+        ri[t].e1 = p2[1];
+      }
+    }
+  };
+  // the raw row data as 8 fp32 values
+  auto as_v8 = [&](const RowIn& ri) -> V8 {
+    if constexpr (EPI == EPI_RESID16 && is16<TC>()) {
+      typedef typename Op16<TC>::v8 v8;
+      const v8 h = __builtin_bit_cast(v8, ri.d0);
+      return V8{{to_f32(h[0]), to_f32(h[1]), to_f32(h[2]), to_f32(h[3]), to_f32(h[4]), to_f32(h[5]), to_f32(h[6]),
+                 to_f32(h[7])}};
+    } else {
+      return V8{{__uint_as_float(ri.d0[0]), __uint_as_float(ri.d0[1]), __uint_as_float(ri.d0[2]),
+                 __uint_as_float(ri.d0[3]), __uint_as_float(ri.d1[0]), __uint_as_float(ri.d1[1]),
+                 __uint_as_float(ri.d1[2]), __uint_as_float(ri.d1[3])}};
+    }
+  };
+  RowIn rbuf[2][TPC];
+  fetch(0, rbuf[0]);
+  static_for<0, MT>([&](auto I) {
+    constexpr int i = decltype(I)::value;
+    if constexpr (i + 1 < MT) fetch(i + 1, rbuf[(i + 1) & 1]);
+#pragma unroll
+    for (int j = 0; j < NT; ++j)
+      *reinterpret_cast<f32x4*>(Cs + fr * EPAD + j * 16 + 4 * q) = acc[i][j];
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+    for (int t = 0; t < TPC; ++t) {
+      const int rr = t * (64 / CH) + lane / CH;
+      const int row = rbase + i * 16 + rr;  // rows >= M: dropped by the store descriptor
+      const float* src = Cs + rr * EPAD + cc * 8;
+      const float4 a0 = *reinterpret_cast<const float4*>(src), a1 = *reinterpret_cast<const float4*>(src + 4);
+      V8 x{{a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w}};
+      if constexpr (BIAS) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) x.v[e] = add_nc(x.v[e], bias8.v[e]);
+      }
+      const RowIn& ri = rbuf[i & 1][t];
+      if constexpr (EPI == EPI_QKV) {
+        const V8 cs = as_v8(ri);
+        // interleaved pairs (a, b) -> (a c - b s, b c + a s) as packed products and one packed add (each
+        // element rounded as rope_re / rope_im round it), then the q scale on pairs
+#pragma unroll
+        for (int p = 0; p < 4; ++p) {
+          const float c = cs.v[2 * p], sn = cs.v[2 * p + 1];
+          const f32x2 ab = {x.v[2 * p], x.v[2 * p + 1]};
+          f32x2 r;
+          {
+#pragma clang fp contract(off)
+            const f32x2 pc = ab * c, ps = f32x2{ab.y, ab.x} * sn;
+            r = pc + f32x2{-ps.x, ps.y};
+            r = (rope_on ? r : ab) * qsc;  // exact for qsc = 1 (k, v columns)
+          }
+          x.v[2 * p] = r.x;
+          x.v[2 * p + 1] = r.y;
+        }
+        (void)row;
+        store8_rs<TC, AUX>(dst, (uint32_t)(((ps_sq[t] * g.heads + head) * g.seq_len + ps_pos[t]) * 64 + dh), x);
+        advance(ps_sq[t], ps_pos[t]);
+      } else if constexpr (EPI == EPI_RESID || EPI == EPI_RESID16) {
+        V8 c;
+        if constexpr (PREF)
+          c = pre[PREF ? i : 0][PREF ? t : 0];
+        else
+          c = as_v8(ri);
+        const bool keep = !masked || ri.kb;
+        V8 o;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) o.v[e] = resid_add(c.v[e], gate8.v[e], x.v[e], keep);
+        store8_rs<ResT<TC, EPI>, AUX>(dst, (uint32_t)((int64_t)row * g.ldc + col), o);
+      } else if constexpr (EPI == EPI_GELU_TANH || EPI == EPI_GELU_ERF_OP) {
+        if constexpr (EPI == EPI_GELU_TANH && is16<TC>()) {
+#pragma unroll
+          for (int e = 0; e < 8; e += 2) {
+            const f32x2 gv = gelu_tanh_fast2(f32x2{x.v[e], x.v[e + 1]});
+            x.v[e] = gv.x;
+            x.v[e + 1] = gv.y;
+          }
+        } else {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) x.v[e] = EPI == EPI_GELU_ERF_OP ? gelu_erf(x.v[e]) : gelu_tanh(x.v[e]);
+        }
+        store8_rs<TC, AUX>(dst, (uint32_t)((int64_t)row * g.ldc + col), x);
+      } else if constexpr (EPI == EPI_STORE16) {
+        store8_rs<TC, AUX>(dst, (uint32_t)((int64_t)row * g.ldc + col), x);
+      } else if constexpr (EPI == EPI_INPROJ) {
+        // x.W_x^T + P for this branch's row, and for the other branch's row (same x, dit.py:162)
+        V8 o0, o1;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          o0.v[e] = x.v[e] + __uint_as_float(ri.d0[e]);
+          o0.v[e + 4] = x.v[e + 4] + __uint_as_float(ri.d1[e]);
+          o1.v[e] = x.v[e] + __uint_as_float(ri.e0[e]);
+          o1.v[e + 4] = x.v[e + 4] + __uint_as_float(ri.e1[e]);
+        }
+        // rows >= M would land in the second block: drop them explicitly (an offset past the descriptor's
+        // extent, which fast_epi_ok keeps below 0xF0000000 bytes; no 32-bit wrap for either 16-B half)
+        constexpr uint32_t kPast = 0xF0000000u / 4;
+        store8_rs<float, AUX>(dst, row < g.M ? (uint32_t)((int64_t)row * g.ldc + col) : kPast, o0);
+        if (g.dual_rows)
+          store8_rs<float, AUX>(dst, row < g.M ? (uint32_t)((int64_t)(row + g.dual_rows) * g.ldc + col) : kPast, o1);
+      } else {  // EPI_STORE
+        store8_rs<float, AUX>(dst, (uint32_t)((int64_t)row * g.ldc + col), x);
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  });
+}
+template <typename TC, int EPI, int MT, int NT, int WN, int EPAD, bool PREF, int AUX = 0, int PM, int PT>
+F5H_DEV void epilogue_fast(const GemmArgs& g, const f32x4 (&acc)[MT][NT], float* Cs, int rbase, int cbase,
+                           int lane, const V8 (&pre)[PM][PT]) {
+  if (g.bias)
+    epilogue_fast_t<TC, EPI, MT, NT, WN, EPAD, PREF, true, PM, PT, AUX>(g, acc, Cs, rbase, cbase, lane, pre);
+  else
+    epilogue_fast_t<TC, EPI, MT, NT, WN, EPAD, PREF, false, PM, PT, AUX>(g, acc, Cs, rbase, cbase, lane, pre);
+}
+
+// Direct epilogue (round 5; the persistent kernel, whose LDS holds the operand ring only): the MFMAs run with swapped operands (W fragment as A, activation fragment as B),
 // so accumulator acc[i][j] holds C^T: lane l has row 16i + (l & 15) and the FOUR CONSECUTIVE columns
 // 16j + 4(l >> 4) + r (r = 0..3). One v_permlane16_swap per dword between blocks j and j+1 (the odd 16-lane
 // rows of block j trade with the even rows of block j+1) leaves every lane with EIGHT consecutive columns of
@@ -511,96 +733,6 @@ F5H_DEV void epilogue_direct_t(const GemmArgs& g, const f32x4 (&acc)[MT][NT], in
     if constexpr (EPI == EPI_QKV) advance(ps_sq, ps_pos);
   });
 }
-// QKV epilogue through the wave's LDS strip (gemm_kernel): per 16-row strip the accumulators go to LDS (one
-// ds_write_b128 per block: the swapped-operand layout already holds four consecutive columns per lane) and come
-// back by rows, 8 lanes per 64-column head row, so every store instruction writes 8 whole 128-B rows of q/k/v.
-// The direct epilogue's stores cover 16 rows x 64 B each (two instructions per row): measured 28.4 against
-// 26.0 us per C2 QKV launch (profiles/r05_ab_c2_attention_epilogue.txt). Same per-element arithmetic as the
-// direct form (bitwise identical).
-template <typename TC, int MT, int NT, int EPAD, bool BIAS>
-F5H_DEV void epilogue_qkv_strip_t(const GemmArgs& g, const f32x4 (&acc)[MT][NT], float* Cs, int rbase, int cbase,
-                                  int lane) {
-  constexpr int WN = NT * 16, CH = WN / 8, TPC = 16 * CH / 64;
-  static_assert(WN == 64, "a wave's 64 columns are one head");
-  const int fr = lane & 15, q = lane >> 4;
-  const int cc = lane % CH, col = cbase + cc * 8;
-  V8 bias8 = V8{};
-  if constexpr (BIAS) bias8 = load8(g.bias + col);
-  const int inner = g.heads * 64;
-  const int which = __builtin_amdgcn_readfirstlane(fdiv(cbase, inner));
-  const int head = __builtin_amdgcn_readfirstlane((cbase - which * inner) >> 6);
-  const int dh = (col - which * inner) & 63;
-  const bool rope_on = which < 2 && head < g.rope_heads;
-  const float qsc = (which == 0 && g.q_scale != 0.f) ? g.q_scale : 1.f;
-  const __amdgpu_buffer_rsrc_t dst =
-      rsrc_of(which == 0 ? g.q : (which == 1 ? g.k : g.v), (uint64_t)g.M * inner * sizeof(TC));
-  int pf_sq[TPC], pf_pos[TPC], ps_sq[TPC], ps_pos[TPC];
-#pragma unroll
-  for (int t = 0; t < TPC; ++t) {
-    const int row0 = rbase + t * (64 / CH) + lane / CH;
-    pf_sq[t] = ps_sq[t] = fdiv(row0, g.seq_len);
-    pf_pos[t] = ps_pos[t] = row0 - pf_sq[t] * g.seq_len;
-  }
-  auto advance = [&](int& sq, int& pos) {
-    pos += 16;
-    while (pos >= g.seq_len) {
-      pos -= g.seq_len;
-      ++sq;
-    }
-  };
-  u32x4 rp[2][TPC][2];  // RoPE (cos, sin) of the chunk's four pairs, fetched one strip ahead
-  auto fetch = [&](u32x4 (&r)[TPC][2]) {
-#pragma unroll
-    for (int t = 0; t < TPC; ++t) {
-      const u32x4* p = reinterpret_cast<const u32x4*>(g.rope + pf_pos[t] * 32 + (dh >> 1));
-      r[t][0] = p[0];
-      r[t][1] = p[1];
-      advance(pf_sq[t], pf_pos[t]);
-    }
-  };
-  fetch(rp[0]);
-  static_for<0, MT>([&](auto I) {
-    constexpr int i = decltype(I)::value;
-    if constexpr (i + 1 < MT) fetch(rp[(i + 1) & 1]);
-#pragma unroll
-    for (int j = 0; j < NT; ++j) *reinterpret_cast<f32x4*>(Cs + fr * EPAD + j * 16 + 4 * q) = acc[i][j];
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-#pragma unroll
-    for (int t = 0; t < TPC; ++t) {
-      const int rr = t * (64 / CH) + lane / CH;
-      const float* src = Cs + rr * EPAD + cc * 8;
-      const float4 a0 = *reinterpret_cast<const float4*>(src), a1 = *reinterpret_cast<const float4*>(src + 4);
-      V8 x{{a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w}};
-      if constexpr (BIAS) {
-#pragma unroll
-        for (int e = 0; e < 8; ++e) x.v[e] = add_nc(x.v[e], bias8.v[e]);
-      }
-      const u32x4* cs4 = rp[i & 1][t];
-#pragma unroll
-      for (int p = 0; p < 4; ++p) {
-        const float c = __uint_as_float(cs4[p >> 1][2 * (p & 1)]), sn = __uint_as_float(cs4[p >> 1][2 * (p & 1) + 1]);
-        const f32x2 ab = {x.v[2 * p], x.v[2 * p + 1]};
-        f32x2 r;
-        {
-#pragma clang fp contract(off)
-          const f32x2 pc = ab * c, ps = f32x2{ab.y, ab.x} * sn;
-          r = pc + f32x2{-ps.x, ps.y};
-          r = (rope_on ? r : ab) * qsc;  // exact for qsc = 1 (k, v columns)
-        }
-        x.v[2 * p] = r.x;
-        x.v[2 * p + 1] = r.y;
-      }
-      store8_rs<TC>(dst, (uint32_t)(((ps_sq[t] * g.heads + head) * g.seq_len + ps_pos[t]) * 64 + dh), x);
-      advance(ps_sq[t], ps_pos[t]);
-    }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-  });
-}
-
 template <typename TC, int EPI, int MT, int NT, bool PREF, int AUX = 0, int PM, int PT>
 F5H_DEV void epilogue_direct(const GemmArgs& g, const f32x4 (&acc)[MT][NT], int rbase, int cbase, int lane,
                              const V8 (&pre)[PM][PT]) {
@@ -859,14 +991,9 @@ F5H_DEV void gemm_body(const GemmArgs& g, const int b, const int nwg, uint4* lds
   // chunk; measured 9.5 us of a 30.6 us QKV launch before).
   constexpr bool FAST_EPI = FAST && NT % 2 == 0;
   static_assert(FAST_EPI || !PUB, "the chain publishes from the direct epilogue");
-  if constexpr (FAST_EPI && EPI == EPI_QKV && !PUB) {
-    float* Cq = reinterpret_cast<float*>(lds) + wid * 16 * C::EPAD;
-    if (g.bias)
-      epilogue_qkv_strip_t<TC, MT, NT, C::EPAD, true>(g, acc, Cq, m0 + wm * WM, n0 + wn * WN, lane);
-    else
-      epilogue_qkv_strip_t<TC, MT, NT, C::EPAD, false>(g, acc, Cq, m0 + wm * WM, n0 + wn * WN, lane);
-  } else if constexpr (FAST_EPI) {
-    epilogue_direct<TC, EPI, MT, NT, PREF, PUB ? kAuxWT : 0>(g, acc, m0 + wm * WM, n0 + wn * WN, lane, pre);
+  if constexpr (FAST_EPI) {
+    epilogue_fast<TC, EPI, MT, NT, WN, C::EPAD, PREF, PUB ? kAuxWT : 0>(g, acc, Cs, m0 + wm * WM, n0 + wn * WN, lane,
+                                                                         pre);
     if constexpr (PUB) chain_publish(dep, g.M, m0, BM);
   }
   if constexpr (!FAST_EPI) {
@@ -1095,7 +1222,7 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(GemmArgs g) {
     // whole-column tiles: the strip-pipelined epilogue (the generic one below waits out every strip's
     // residual / RoPE loads before its stores: 13-15 us per 256x256 tile at C3, profiles/r03_timeline_c3.txt)
     const V8 none[1][1] = {};
-    epilogue_direct<TC, EPI, MT, NT, false>(g, acc, rbase, cbase, lane, none);
+    epilogue_fast<TC, EPI, MT, NT, WN, C::EPAD, false>(g, acc, Cs, rbase, cbase, lane, none);
   } else {
 #pragma unroll
   for (int i = 0; i < MT; ++i) {
@@ -1536,7 +1663,7 @@ __global__ __launch_bounds__(512, 1) void gemm_8p_kernel(GemmArgs g) {
     const int rbase = m0 + ha * 128 + wr * 64, cbase = n0 + hb * 128 + wc * QW;
     if constexpr (FAST) {
       const V8 none[1][1] = {};
-      epilogue_direct<TC, EPI, 4, 2, false>(g, acc[ha][hb], rbase, cbase, lane, none);
+      epilogue_fast<TC, EPI, 4, 2, QW, EPAD, false>(g, acc[ha][hb], Cs, rbase, cbase, lane, none);
     } else {
       constexpr int CH = QW / 8;
 #pragma unroll
