@@ -878,21 +878,19 @@ F5H_DEV void gemm_body(const GemmArgs& g, const int b, const int nwg, uint4* lds
   // operand stages (so they do not delay stage 0: the first wait leaves them in flight, the second
   // retires them), and the epilogue's read-modify-write does not expose a dependent HBM/MALL round
   // trip. Register budget: small tiles only.
-  // (the direct epilogue's layout: lane row 16i + (lane & 15), its 8-column chunk coff within each pair of
-  // 16-column blocks)
-  constexpr int NPAIR = NT / 2;
-  constexpr bool PREF = (EPI == EPI_RESID || EPI == EPI_RESID16) && is16<TC>() && NT % 2 == 0 &&
-                        MT * NPAIR * 8 <= 32;
-  V8 pre[PREF ? MT : 1][PREF ? NPAIR : 1];
+  // (the strip epilogue's layout: chunk t of strip i is row 16i + (64t + lane) / CH_, 8-column chunk (64t + lane) % CH_)
+  constexpr int CH_ = WN / 8, TPS = 16 * CH_ / 64;
+  constexpr bool PREF = (EPI == EPI_RESID || EPI == EPI_RESID16) && is16<TC>() && (16 * CH_) % 64 == 0 &&
+                        MT * TPS * 8 <= 32;
+  V8 pre[PREF ? MT : 1][PREF ? TPS : 1];
   if constexpr (PREF) {
     const ResT<TC, EPI>* Cp = reinterpret_cast<const ResT<TC, EPI>*>(g.resid ? g.resid : g.C);
-    const int fr_ = lane & 15, q_ = lane >> 4;
-    const int coff = 16 * (q_ & 1) + 8 * (q_ >> 1);
 #pragma unroll
     for (int i = 0; i < MT; ++i)
 #pragma unroll
-      for (int t = 0; t < NPAIR; ++t) {
-        const int row = m0 + wm * WM + i * 16 + fr_, col = n0 + wn * WN + 32 * t + coff;
+      for (int t = 0; t < TPS; ++t) {
+        const int idx = t * 64 + lane, rr = idx / CH_, cc = idx % CH_;
+        const int row = m0 + wm * WM + i * 16 + rr, col = n0 + wn * WN + cc * 8;
         const bool ok = row < g.M && col + 8 <= g.N && g.ldc % 4 == 0;
         // unconditional (a select on the address, no branch): the loads issue back to back
         // (a branch per load made hipcc wait for each one in turn); unused when !ok
@@ -900,7 +898,7 @@ F5H_DEV void gemm_body(const GemmArgs& g, const int b, const int nwg, uint4* lds
       }
   }
 
-  constexpr int NPRE = PREF ? MT * NPAIR : 0;  // residual loads issued behind the first stages
+  constexpr int NPRE = PREF ? MT * TPS : 0;  // residual loads issued behind the first stages
   for (int kt = 0; kt < nk; ++kt) {
     // stage kt has landed for THIS wave once at most the younger in-flight stages remain;
     // the barrier then publishes every wave's part of it
