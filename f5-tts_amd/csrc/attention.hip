@@ -76,18 +76,14 @@ F5H_DEV void attn_block(int& qb, int& bh) {
 
 // RSM: row sums on the matrix pipe (l^T += ones . P^T, one 32x32x16 MFMA per 16-key chunk) instead of 16 packed
 // VALU adds per tile (F5H_ATTN_ROWSUM=mfma; an A/B switch, results agree to rounding)
-// STAG: waves 4-7 (the second wave of every SIMD) run each tile's exp2 / P.V half one tile late, after the next
-// barrier and before that tile's Q.K^T half, so that on every SIMD one wave's MFMAs meet the other wave's exp2s
-// (MI355X_MICROARCH.md 'Two waves per SIMD', item 9: two waves of the same program behind one barrier per block
-// run in lock-step). Needs a fifth ring slot (the late half reads tile t-1's V while tile t+3 lands).
-template <typename T, bool PRESCALED, int NW, bool RSM, bool STAG = false>
+template <typename T, bool PRESCALED, int NW, bool RSM>
 __global__ __launch_bounds__(64 * NW, 8 / NW) void attn16_kernel(AttnArgs a) {
   typedef Op16<T> OP;
   typedef typename OP::v8 v8;
   typedef typename OP::v4 v4;
   const ProbeT probe_t = probe_enter(a.probe);
   constexpr int TILE_B = 2 * 64 * 128;  // K + V tile bytes (64 keys x 64 dh x 2 B each)
-  constexpr int NS = STAG ? 5 : 4;      // LDS ring: one tile read while three are in flight (+1: STAG)
+  constexpr int NS = 4;                 // LDS ring: one tile read while three are in flight
   constexpr int CPW = 512 / (64 * NW);  // 16-B chunks of one K (or V) tile per lane
   constexpr float THR = 8.f;
   static_assert(CPW * 64 * NW == 512, "whole DMA rounds");
@@ -224,9 +220,9 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn16_kernel(AttnArgs a) {
   // every P). SAFE (the rerun of a workgroup where a row failed that check, i.e. some score ran more than
   // log2(LMAX) above its row's first-tile max): the lazy running max of cdna_hip_programming.md T13 -- per
   // tile row max, re-base when it exceeds m_run by more than THR.
-  f32x16 sacc[2];  // S^T - m_run of the tile between its two halves (STAG: across the next barrier)
+  f32x16 sacc[2];  // S^T - m_run of the tile between its two halves
   // tile kt landed for this wave's own DMA (tile kt+1 may stay in flight); the barrier publishes every wave's
-  // part of it and retires all reads of slot (kt+3)%NS (= tile kt-1; STAG: tile kt-2).
+  // part of it and retires all reads of slot (kt+3)%NS (= tile kt-1).
   auto tile_wait = [&](const int kt) __attribute__((always_inline)) {
     if (kt + 2 < ntile)
       asm volatile("s_waitcnt vmcnt(%0)" ::"i"(4 * CPW) : "memory");
@@ -242,13 +238,12 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn16_kernel(AttnArgs a) {
     if (FIRST && !SAFE) probe_mark(a.probe, probe_t, 1);
     constexpr int slot = decltype(SLOT)::value;
     constexpr uint32_t so = (uint32_t)(slot * TILE_B);  // ring slot offset: an immediate of every LDS read
-    constexpr uint32_t sb = so >= 65536 ? 65536u : 0u;  // (16-bit immediates: the fifth slot from a second base)
 
     u32x4 kf[2][4];
     static_for<0, 4>([&](auto KS) {
       constexpr int ks = decltype(KS)::value;
-      kf[0][ks] = lds_b128<so - sb>(kaddr[ks] + sb);
-      kf[1][ks] = lds_b128<so - sb + 4096>(kaddr[ks] + sb);
+      kf[0][ks] = lds_b128<so>(kaddr[ks]);
+      kf[1][ks] = lds_b128<so + 4096>(kaddr[ks]);
     });
     if (kt + 3 < ntile) dma((slot + 3) % NS, kt + 3, true);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -316,7 +311,6 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn16_kernel(AttnArgs a) {
   auto tile_pv = [&](auto SLOT) __attribute__((always_inline)) {
     constexpr int slot = decltype(SLOT)::value;
     constexpr uint32_t so = (uint32_t)(slot * TILE_B);
-    constexpr uint32_t sb = so >= 65536 ? 65536u : 0u;
     uint2 vf[2][2][2][2];
     auto vread = [&](auto U) {
       constexpr int u = decltype(U)::value;
@@ -324,8 +318,8 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn16_kernel(AttnArgs a) {
         constexpr int t = decltype(TT)::value;
         static_for<0, 2>([&](auto S) {
           constexpr int sx = decltype(S)::value;
-          vf[u][t][sx][0] = lds_tr_b64<so - sb + (32 * t + 16 * sx) * 128>(vaddr[u][0] + sb);
-          vf[u][t][sx][1] = lds_tr_b64<so - sb + (32 * t + 16 * sx) * 128>(vaddr[u][1] + sb);
+          vf[u][t][sx][0] = lds_tr_b64<so + (32 * t + 16 * sx) * 128>(vaddr[u][0]);
+          vf[u][t][sx][1] = lds_tr_b64<so + (32 * t + 16 * sx) * 128>(vaddr[u][1]);
         });
       });
     };
@@ -392,13 +386,6 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn16_kernel(AttnArgs a) {
     tile_qk(SLOT, FIRST_, SAFE_, kt);
     tile_pv(SLOT);
   };
-  // STAG's late half (waves 4-7): tile kt's P.V after barrier kt + 1, before tile kt + 1's Q.K^T
-  auto tile_late = [&](auto SLOT, auto SAFE_, const int kt) __attribute__((always_inline)) {
-    constexpr int slot = decltype(SLOT)::value;
-    tile_wait(kt);
-    if (kt >= 1) tile_pv(std::integral_constant<int, (slot + NS - 1) % NS>{});
-    tile_qk(SLOT, std::false_type{}, SAFE_, kt);
-  };
   auto pass = [&](auto SAFE_) __attribute__((always_inline)) {
     if (wave_dead) {
       for (int kt = 0; kt < ntile; ++kt) {
@@ -411,21 +398,6 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn16_kernel(AttnArgs a) {
         __builtin_amdgcn_s_barrier();
         if (kt + 3 < ntile) dma((kt + 3) % NS, kt + 3, true);
       }
-    } else if (STAG && wid_s >= 4) {
-      if (ntile > 0) {
-        tile_wait(0);
-        tile_qk(std::integral_constant<int, 0>{}, IT{}, SAFE_, 0);
-      }
-      for (int kt0 = 0; kt0 < ntile; kt0 += NS) {
-        static_for<0, NS>([&](auto S) {
-          const int kt = kt0 + decltype(S)::value;
-          if (kt >= 1 && kt < ntile) tile_late(S, SAFE_, kt);
-        });
-      }
-      // the last tile's P.V (its slot is a constant of each branch)
-      static_for<0, NS>([&](auto S) {
-        if (ntile > 0 && (ntile - 1) % NS == decltype(S)::value) tile_pv(S);
-      });
     } else {
       if (ntile > 0) tile(std::integral_constant<int, 0>{}, IT{}, SAFE_, 0);
       for (int kt0 = 0; kt0 < ntile; kt0 += NS) {
@@ -576,14 +548,8 @@ static void launch16(const AttnArgs& a, hipStream_t st) {
     const char* v = getenv("F5H_ATTN_ROWSUM");
     return v && !strcmp(v, "mfma");
   }();
-  static const bool stag = [] {
-    const char* v = getenv("F5H_ATTN_STAGGER");
-    return v && *v == '1';
-  }();
   if (a.prescaled) {
-    if (stag)
-      hipLaunchKernelGGL((attn16_kernel<T, true, NW, false, true>), grid, dim3(64 * NW), 0, st, a);
-    else if (rsm)
+    if (rsm)
       hipLaunchKernelGGL((attn16_kernel<T, true, NW, true>), grid, dim3(64 * NW), 0, st, a);
     else
       hipLaunchKernelGGL((attn16_kernel<T, true, NW, false>), grid, dim3(64 * NW), 0, st, a);

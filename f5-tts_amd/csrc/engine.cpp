@@ -118,9 +118,9 @@ struct f5h_engine {
   // skip the dead pad-row work of the batch path (attention query blocks and out-proj row tiles of padding
   // only): f5h_set_pad_skip, env F5H_NO_PAD_SKIP=1 at creation turns it off. Bitwise identical results.
   int pad_skip = 1;
-  // In-launch phase chain of the DiT block-step's row-local seams (chain.hip): f5h_set_chain, env F5H_CHAIN=1 at
-  // creation. Bitwise identical results.
-  int chain = 0;
+  // In-launch phase chain of the DiT block-step's row-local seams (chain.hip): f5h_set_chain, env F5H_CHAIN=0 at
+  // creation turns it off. Bitwise identical results.
+  int chain = 1;
   uint64_t use_ctr = 0;
   int64_t n_captures = 0, n_replays = 0;
   // probe
@@ -983,7 +983,7 @@ int f5h_engine_create_views(const f5h_arch* arch, const f5h_tensor_view* weights
   if (const char* gv = getenv("F5H_GRAPH")) e->graph_mode = atoi(gv) ? 1 : 0;
   if (const char* sv = getenv("F5H_SPLIT_CFG")) e->split_cfg = std::min(2, std::max(0, atoi(sv)));
   if (const char* pv = getenv("F5H_NO_PAD_SKIP")) e->pad_skip = (*pv == '1') ? 0 : 1;
-  if (const char* cv = getenv("F5H_CHAIN")) e->chain = (*cv == '1') ? 1 : 0;
+  if (const char* cv = getenv("F5H_CHAIN")) e->chain = (*cv == '0') ? 0 : 1;
   // device views are read on the engine's non-blocking stream: order it behind the null stream (so behind
   // every blocking stream's queued work, the ordering the packing had when it ran on the null stream); work
   // on other non-blocking streams must be complete (f5h.h)
@@ -1632,8 +1632,8 @@ int f5h_op_linear(void* stream, int32_t compute, int32_t M, int32_t N, int32_t K
 }
 
 int f5h_gemm_force_config(int32_t cfg) {
-  if (cfg != -1 && cfg != 0 && cfg != 1 && cfg != 5 && (cfg < 11 || cfg > 16))
-    return fail(F5H_EINVAL, "gemm config must be -1, 0, 1, 5 or 11-16");
+  if (cfg != -1 && cfg != 0 && cfg != 1 && cfg != 5 && cfg != 11 && cfg != 12 && cfg != 13)
+    return fail(F5H_EINVAL, "gemm config must be -1, 0, 1, 5, 11, 12 or 13");
   gemm_force_config(cfg);
   g_kernel_epoch.fetch_add(1);
   return 0;

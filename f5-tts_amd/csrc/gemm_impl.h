@@ -1785,24 +1785,6 @@ static hipError_t launch_t(const GemmArgs& a, hipStream_t st) {
     default:
       if constexpr (is16<TC>()) {
         if (a.K % 64) return hipErrorInvalidValue;  // whole K64 tiles
-        // 14-16: one-block-per-CU ping-pong tiles for the single-utterance shapes (C2: 240 tiles fill the 256 CUs
-        // once), built for the C2 hot epilogues only: 128x128 (N = 1024), 256x128 (FFN1), 192x256 (QKV)
-        // (and EPI_STORE, which the op-level tests drive); other epilogues take cfg 0
-        constexpr bool C2E = EPI == EPI_QKV || EPI == EPI_RESID16 || EPI == EPI_RESID || EPI == EPI_GELU_TANH ||
-                             EPI == EPI_STORE;
-        if (cfg == 14 || cfg == 15 || cfg == 16) {
-          if constexpr (C2E) {
-            if (cfg == 14)
-              launch_pp<TC, EPI, 128, 128, 2, 2, 2, 3>(a, st);
-            else if (cfg == 15)
-              launch_pp<TC, EPI, 256, 128, 2, 2, 1, 3>(a, st);
-            else
-              launch_pp<TC, EPI, 192, 256, 1, 4, 1, 3>(a, st);
-          } else {
-            launch_cfg<TC, EPI, 64, 128, 2, 2, 3>(a, st);
-          }
-          break;
-        }
         if (cfg != 11 && cfg != 12 && cfg != 13) return hipErrorInvalidValue;
         if (cfg == 11)
           launch_pp<TC, EPI, 256, 256, 1, 4, 1, 3>(a, st);

@@ -128,7 +128,7 @@ class Engine:
 
     def set_chain(self, on: bool):
         """Run each DiT layer's row-local seams (out-proj .. next QKV) as one phase-chain launch (16-bit DiT
-        path without row masks; f5h_set_chain). Results are bitwise identical either way."""
+        path without row masks; f5h_set_chain; default on). Results are bitwise identical either way."""
         _lib.check(_lib.lib().f5h_set_chain(self._h, int(bool(on))), "set_chain")
 
     def graph_stats(self):

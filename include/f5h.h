@@ -215,8 +215,8 @@ int f5h_graph_stats(f5h_engine* eng, int64_t* captures, int64_t* replays, int32_
 int f5h_set_pad_skip(f5h_engine* eng, int32_t enable);
 /* 16-bit DiT path without row masks: run each layer's out-proj, LayerNorm, FFN1, FFN2 and the next layer's
  * LayerNorm + QKV (modules.py:743-757) as ONE launch whose phases hand 64-row groups to each other through
- * arrival counters (chain.hip, DESIGN.md §3 'Phase chain'), instead of six launches. 1 or 0 (default; env
- * F5H_CHAIN=1 at creation: 1). Bitwise identical results. */
+ * arrival counters (chain.hip, DESIGN.md §3 'Phase chain'), instead of six launches. 1 (default) or 0 (env
+ * F5H_CHAIN=0 at creation: 0). Bitwise identical results. */
 int f5h_set_chain(f5h_engine* eng, int32_t enable);
 /* Test hook: *launches = phase-chain launches this process has enqueued (eager launches and graph captures);
  * *fault = 1 if one of them gave up waiting for a producer (a bounded wait that should never expire; its
@@ -235,7 +235,7 @@ int f5h_op_attention(void* stream, int32_t compute, int32_t S, int32_t H, int32_
                      void* workspace, size_t workspace_bytes);
 
 /* Tuning/test hook: pin the 16-bit GEMM tile configuration for all later launches in this
- * process (0, 1, 5, 11-16; 14-16 only for the QKV, residual and GELU epilogues), or -1 to restore the automatic per-shape choice. */
+ * process (0, 1, 5, 11, 12, 13), or -1 to restore the automatic per-shape choice. */
 int f5h_gemm_force_config(int32_t cfg);
 /* Test hook: on != 0 makes every later 16-bit attention launch of this process rerun each workgroup's key
  * loop in its lazy-running-max form (the path a row takes when a score runs far above its first tile's max;

@@ -621,6 +621,6 @@ def test_phase_chain_bitwise_equal(compute):
                 assert torch.equal(outs[mode][0], outs["plain"][0]), (total, mode)
                 assert torch.equal(outs[mode][1], outs["plain"][1]), (total, mode)
     finally:
-        eng.set_chain(False)
+        eng.set_chain(True)
         eng.set_graph_mode(True)
         eng.set_cfg_streams(0)

@@ -67,8 +67,7 @@ def test_op_linear(compute, tol, M, N, K):
     assert err < tol, err
 
 
-GEMM_CONFIGS = [0, 1, 5, 11, 12, 13, 14, 15, 16]  # 11: ping-pong 8-wave 256x256; 12: 8-phase 256x256; 13: persistent
-# ping-pong; 14-16: one-block-per-CU ping-pong 128x128, 256x128, 192x256 (hot epilogues + EPI_STORE; others take cfg 0)
+GEMM_CONFIGS = [0, 1, 5, 11, 12, 13]  # 11: ping-pong 8-wave 256x256; 12: 8-phase 256x256; 13: persistent ping-pong
 if os.environ.get("F5H_TEST_GEMM_CFGS"):  # tuning runs: check extra configurations too
     GEMM_CONFIGS = [int(c) for c in os.environ["F5H_TEST_GEMM_CFGS"].split(",")]
 

@@ -21,8 +21,9 @@ for _k in (128, 256, 512, 2048, 4096):  # K sweeps at the C2 output shapes: fixe
     SHAPES[f"c2_out_k{_k}"] = (3752, 1024, _k)
     SHAPES[f"c2_qkv_k{_k}"] = (3752, 3072, _k)
 CFGS = {0: (64, 128, 256), 1: (128, 128, 256), 5: (192, 128, 256), 11: (256, 256, 512), 12: (256, 256, 512),
-        13: (256, 256, 512), 14: (128, 128, 512), 15: (256, 128, 512), 16: (192, 256, 512)}
-# 13: persistent (one block per CU); 14-16: one-block-per-CU ping-pong tiles for the C2 shapes
+        13: (256, 256, 512)}  # 13: persistent (one block per CU)
+# round 5 also timed one-block-per-CU ping-pong tiles at the C2 shapes (128x128, 256x128, 192x256 as cfg 14-16):
+# slower than the picks on every C2 GEMM (profiles/r05_gemm_tune_c2_pp.txt), removed
 # round 3 also timed register-staged intake (cfg 40-45) and K32-stage deeper rings for 192x128 / 128x128
 # (cfg 6-8): slower on every C2 and C3 shape (profiles/r03_gemm_tune_rs_c2.txt, r03_gemm_tune_k32.txt)
 # round 2 also timed 8-wave one-block-per-CU tiles (128x256, 192x256, 256x128, 128x128, 256x256, 256x192),

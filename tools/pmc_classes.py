@@ -55,10 +55,14 @@ def load(path, counter):
 def classify(disp):
     cls = {}
     for i, (_, name, _) in enumerate(disp):
+        if "chain_kernel" in name:  # the phase chain (chain.hip): out-proj .. next QKV as one launch
+            cls[i] = "chain"
+    for i, (_, name, _) in enumerate(disp):
         if "attn16" in name or "attn_f32" in name:
             cls[i] = "attention"
             for off, c in ORDER.items():
-                if 0 <= i + off < len(disp) and ("gemm" in disp[i + off][1]) == (c in GEMMS):
+                if 0 <= i + off < len(disp) and "chain_kernel" not in disp[i + off][1] and \
+                        ("gemm" in disp[i + off][1]) == (c in GEMMS):
                     cls.setdefault(i + off, c)
         elif "conv16_kernel" in name or "conv_kernel" in name:  # ConvPositionEmbedding layers (conv.hip)
             cls[i] = "conv"
