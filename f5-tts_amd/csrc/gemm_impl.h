@@ -320,7 +320,10 @@ F5H_DEV void store8_rs(__amdgpu_buffer_rsrc_t r, uint32_t elem, const V8& x) {
 // before it counts in the same vmcnt: at C3 such waits made the 256x256 ping-pong epilogue 13-15 us per
 // tile (profiles/r03_timeline_c3.txt). rbase/cbase: the sub-tile's first row/column.
 // Shared by gemm_kernel and gemm_pp_kernel.
-template <typename TC, int EPI, int MT, int NT, int WN, int EPAD, bool PREF, bool BIAS, int PM, int PT, int AUX = 0>
+// PD: strips of row data fetched ahead (1: the next strip's; the 256x256 residual epilogues fetch all MT up
+// front, their loads otherwise exposing most of a memory round trip per strip)
+template <typename TC, int EPI, int MT, int NT, int WN, int EPAD, bool PREF, bool BIAS, int PM, int PT, int AUX = 0,
+          int PD = 1>
 F5H_DEV void epilogue_fast_t(const GemmArgs& g, const f32x4 (&acc)[MT][NT], float* Cs, int rbase, int cbase,
                              int lane, const V8 (&pre)[PM][PT]) {
   constexpr int CH = WN / 8;          // 8-column chunks per strip row
@@ -424,11 +427,12 @@ F5H_DEV void epilogue_fast_t(const GemmArgs& g, const f32x4 (&acc)[MT][NT], floa
                  __uint_as_float(ri.d1[2]), __uint_as_float(ri.d1[3])}};
     }
   };
-  RowIn rbuf[2][TPC];
-  fetch(0, rbuf[0]);
+  constexpr int RB = PD + 1;  // row-data ring
+  RowIn rbuf[RB][TPC];
+  static_for<0, (PD < MT ? PD : MT)>([&](auto F) { fetch(decltype(F)::value, rbuf[decltype(F)::value % RB]); });
   static_for<0, MT>([&](auto I) {
     constexpr int i = decltype(I)::value;
-    if constexpr (i + 1 < MT) fetch(i + 1, rbuf[(i + 1) & 1]);
+    if constexpr (i + PD < MT) fetch(i + PD, rbuf[(i + PD) % RB]);
 #pragma unroll
     for (int j = 0; j < NT; ++j)
       *reinterpret_cast<f32x4*>(Cs + fr * EPAD + j * 16 + 4 * q) = acc[i][j];
@@ -446,7 +450,7 @@ F5H_DEV void epilogue_fast_t(const GemmArgs& g, const f32x4 (&acc)[MT][NT], floa
 #pragma unroll
         for (int e = 0; e < 8; ++e) x.v[e] = add_nc(x.v[e], bias8.v[e]);
       }
-      const RowIn& ri = rbuf[i & 1][t];
+      const RowIn& ri = rbuf[i % RB][t];
       if constexpr (EPI == EPI_QKV) {
         const V8 cs = as_v8(ri);
         // interleaved pairs (a, b) -> (a c - b s, b c + a s) as packed products and one packed add (each
@@ -519,13 +523,13 @@ F5H_DEV void epilogue_fast_t(const GemmArgs& g, const f32x4 (&acc)[MT][NT], floa
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   });
 }
-template <typename TC, int EPI, int MT, int NT, int WN, int EPAD, bool PREF, int AUX = 0, int PM, int PT>
+template <typename TC, int EPI, int MT, int NT, int WN, int EPAD, bool PREF, int AUX = 0, int PD = 1, int PM, int PT>
 F5H_DEV void epilogue_fast(const GemmArgs& g, const f32x4 (&acc)[MT][NT], float* Cs, int rbase, int cbase,
                            int lane, const V8 (&pre)[PM][PT]) {
   if (g.bias)
-    epilogue_fast_t<TC, EPI, MT, NT, WN, EPAD, PREF, true, PM, PT, AUX>(g, acc, Cs, rbase, cbase, lane, pre);
+    epilogue_fast_t<TC, EPI, MT, NT, WN, EPAD, PREF, true, PM, PT, AUX, PD>(g, acc, Cs, rbase, cbase, lane, pre);
   else
-    epilogue_fast_t<TC, EPI, MT, NT, WN, EPAD, PREF, false, PM, PT, AUX>(g, acc, Cs, rbase, cbase, lane, pre);
+    epilogue_fast_t<TC, EPI, MT, NT, WN, EPAD, PREF, false, PM, PT, AUX, PD>(g, acc, Cs, rbase, cbase, lane, pre);
 }
 
 // Direct epilogue (round 5; the persistent kernel, whose LDS holds the operand ring only): the MFMAs run with swapped operands (W fragment as A, activation fragment as B),
@@ -1220,7 +1224,8 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(GemmArgs g) {
     // whole-column tiles: the strip-pipelined epilogue (the generic one below waits out every strip's
     // residual / RoPE loads before its stores: 13-15 us per 256x256 tile at C3, profiles/r03_timeline_c3.txt)
     const V8 none[1][1] = {};
-    epilogue_fast<TC, EPI, MT, NT, WN, C::EPAD, false>(g, acc, Cs, rbase, cbase, lane, none);
+    constexpr int PD = EPI == EPI_RESID16 ? MT : (EPI == EPI_RESID ? MT / 2 : 1);  // fp32 rows: half (registers)
+    epilogue_fast<TC, EPI, MT, NT, WN, C::EPAD, false, 0, PD>(g, acc, Cs, rbase, cbase, lane, none);
   } else {
 #pragma unroll
   for (int i = 0; i < MT; ++i) {
