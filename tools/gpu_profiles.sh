@@ -43,3 +43,6 @@ if [ "${CHAIN_TRACE:-1}" = 1 ] && echo " ${CONFIGS:-c2} " | grep -q " c2 "; then
   (cd tools && python class_profile.py trace $O/tr_chain/run_kernel_trace.csv c2 $O/${P}_rocprof_chain_c2.json > /dev/null) \
     && echo "chain trace ok" || exit 1
 fi
+# keep the summaries (and the rocprof stats); the per-dispatch CSVs would exceed what a call may bring back
+find $O -name "*_kernel_trace.csv" -delete -o -name "*_counter_collection.csv" -delete
+du -sh $PWD/gpurun_out

@@ -17,3 +17,4 @@ for c in FETCH_SIZE WRITE_SIZE; do
 done
 python tools/pmc_classes.py $O/${CFG}_FETCH_SIZE/run_counter_collection.csv \
   $O/${CFG}_WRITE_SIZE/run_counter_collection.csv $OUT $CFG && echo "pmc ok"
+[ -n "$KEEP_CSV" ] || find $O -name "*_counter_collection.csv" -delete
