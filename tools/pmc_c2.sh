@@ -16,5 +16,6 @@ for c in FETCH_SIZE WRITE_SIZE; do
     python tools/trace_c2.py run $CFG > $O/pmc_${CFG}_$c.log 2>&1 || { echo "pmc $c failed"; exit 1; }
 done
 python tools/pmc_classes.py $O/${CFG}_FETCH_SIZE/run_counter_collection.csv \
-  $O/${CFG}_WRITE_SIZE/run_counter_collection.csv $OUT $CFG && echo "pmc ok"
+  $O/${CFG}_WRITE_SIZE/run_counter_collection.csv $OUT $CFG || exit 1
+echo "pmc ok"
 [ -n "$KEEP_CSV" ] || find $O -name "*_counter_collection.csv" -delete
