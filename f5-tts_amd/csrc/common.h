@@ -279,15 +279,6 @@ F5H_DEV int spread8(int r, int n) {
   return i * 8 + c;
 }
 
-// XCD-contiguous logical block id (cdna_hip_programming.md T1, bijective form): the hardware deals workgroups
-// round-robin over the 8 XCDs, so blocks b and b + 8 share one; this gives XCD x (blocks b % 8 == x) the x-th
-// contiguous chunk of [0, nwg). Row kernels use it so that an XCD handles the contiguous row range the GEMM
-// launches around them give that XCD (their tile remap is the same), and reads rows its own L2 wrote.
-F5H_DEV int xcd_block(int b, int nwg) {
-  const int xq = nwg >> 3, xr = nwg & 7, xcd = b & 7;
-  return (xcd < xr ? xcd * (xq + 1) : xr * (xq + 1) + (xcd - xr) * xq) + (b >> 3);
-}
-
 F5H_DEV __amdgpu_buffer_rsrc_t rsrc_of(const void* p, uint64_t bytes) {
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), 0, (int)(uint32_t)bytes, 0x00020000);
 }

@@ -144,7 +144,7 @@ __global__ __launch_bounds__(256) void ln_mod_kernel(const TI* h, int M, int d, 
                                                      const float* scale, TO* out) {
   constexpr bool FIXED = NV > 0;
   constexpr int V = FIXED ? NV : MAXV;
-  const int row = xcd_block(blockIdx.x, gridDim.x) * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
   if (row >= M) return;
   const TI* x = h + (int64_t)row * d;
   const float4* sh = reinterpret_cast<const float4*>(shift);
@@ -167,7 +167,7 @@ template <typename T>
 __global__ __launch_bounds__(256) void ln_mod16_kernel(const T* h, int M, const float* shift, const float* scale,
                                                        T* out) {
   constexpr int d = 1024;
-  const int row = xcd_block(blockIdx.x, gridDim.x) * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
   if (row >= M) return;
   const uint4* x = reinterpret_cast<const uint4*>(h + (int64_t)row * d);
   const float4* sh = reinterpret_cast<const float4*>(shift);
@@ -226,7 +226,7 @@ template <typename TO, int NV, typename TI = float>
 __global__ __launch_bounds__(256) void rms_kernel(const TI* h, int M, int d, const float* g, TO* out) {
   constexpr bool FIXED = NV > 0;
   constexpr int V = FIXED ? NV : MAXV;
-  const int row = xcd_block(blockIdx.x, gridDim.x) * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
   if (row >= M) return;
   const TI* x = h + (int64_t)row * d;
   const float4* gg = reinterpret_cast<const float4*>(g);
@@ -257,7 +257,7 @@ template <typename T>
 __global__ __launch_bounds__(256) void rms16_kernel(const T* h, int M, const float* g, T* out) {
   typedef typename Op16<T>::v8 v8;
   constexpr int d = 1024;
-  const int row = xcd_block(blockIdx.x, gridDim.x) * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
   if (row >= M) return;
   const uint4* x = reinterpret_cast<const uint4*>(h + (int64_t)row * d);
   const float4* gg = reinterpret_cast<const float4*>(g);

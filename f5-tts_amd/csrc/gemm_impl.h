@@ -320,8 +320,8 @@ F5H_DEV void store8_rs(__amdgpu_buffer_rsrc_t r, uint32_t elem, const V8& x) {
 // before it counts in the same vmcnt: at C3 such waits made the 256x256 ping-pong epilogue 13-15 us per
 // tile (profiles/r03_timeline_c3.txt). rbase/cbase: the sub-tile's first row/column.
 // Shared by gemm_kernel and gemm_pp_kernel.
-// PD: strips of row data fetched ahead (1: the next strip's; the 256x256 residual epilogues fetch all MT up
-// front, their loads otherwise exposing most of a memory round trip per strip)
+// PD: strips of row data fetched ahead (1: the next strip's; fetching every strip's residual up front in the 256x256
+// ping-pong kernel measured equal at C4/C5, profiles/r05_ab_c4_c5_resid_prefetch.txt)
 template <typename TC, int EPI, int MT, int NT, int WN, int EPAD, bool PREF, bool BIAS, int PM, int PT, int AUX = 0,
           int PD = 1>
 F5H_DEV void epilogue_fast_t(const GemmArgs& g, const f32x4 (&acc)[MT][NT], float* Cs, int rbase, int cbase,
@@ -1224,8 +1224,7 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(GemmArgs g) {
     // whole-column tiles: the strip-pipelined epilogue (the generic one below waits out every strip's
     // residual / RoPE loads before its stores: 13-15 us per 256x256 tile at C3, profiles/r03_timeline_c3.txt)
     const V8 none[1][1] = {};
-    constexpr int PD = EPI == EPI_RESID16 ? MT : (EPI == EPI_RESID ? MT / 2 : 1);  // fp32 rows: half (registers)
-    epilogue_fast<TC, EPI, MT, NT, WN, C::EPAD, false, 0, PD>(g, acc, Cs, rbase, cbase, lane, none);
+    epilogue_fast<TC, EPI, MT, NT, WN, C::EPAD, false>(g, acc, Cs, rbase, cbase, lane, none);
   } else {
 #pragma unroll
   for (int i = 0; i < MT; ++i) {
