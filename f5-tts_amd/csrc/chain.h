@@ -43,6 +43,7 @@ F5H_DEV void chain_wait(const ChainDep& d, int M, int r0, int nrows) {
     }
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (d.tl && threadIdx.x == 0) d.tl[1] = wall_clock64();
   }
   __syncthreads();
 }
@@ -51,6 +52,7 @@ F5H_DEV void chain_wait(const ChainDep& d, int M, int r0, int nrows) {
 F5H_DEV void chain_publish(const ChainDep& d, int M, int r0, int nrows) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every wave: its stores have left
   __syncthreads();
+  if (d.tl && threadIdx.x == 0) d.tl[2] = wall_clock64();
   if (threadIdx.x == 0) {
     const int g0 = r0 / kChainRows, g1 = (min(r0 + nrows, M) - 1) / kChainRows;
     for (int gi = g0; gi <= g1; ++gi) __hip_atomic_fetch_add(d.pub + gi, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);

@@ -546,7 +546,7 @@ static void layout(const f5h_engine* e, WS& ws, Bufs& b, int B, int N, int nfe, 
 }
 
 // ---------------------------------------------------------------- probe
-enum { KC_FFN1 = 0, KC_ATTN = 1, KC_QKV = 2, KC_FFN2 = 3, KC_CONV = 4, KC_OUT = 5, KC_NORM = 6 };
+enum { KC_FFN1 = 0, KC_ATTN = 1, KC_QKV = 2, KC_FFN2 = 3, KC_CONV = 4, KC_OUT = 5, KC_NORM = 6, KC_CHAIN = 7 };
 // Times one launch site when its kernel class is probed. With `kp` the kernel stamps itself
 // (GemmArgs/AttnArgs::probe); without, stamp kernels bracket the launch.
 struct ProbeScope {
@@ -789,7 +789,8 @@ static int backbone_part(Ctx& c, int s0, int ns, hipStream_t st) {
   // while a chained class is probed (its launches are timed one by one).
   const int part = s0 ? 1 : 0;
   const bool chain_on = dit && r16 && do_ln && e->chain && !keep && d == 1024 && b.chain[part] &&
-                        (e->probe_class < 0 || e->probe_class == KC_ATTN || e->probe_class == KC_CONV);
+                        (e->probe_class < 0 || e->probe_class == KC_ATTN || e->probe_class == KC_CONV ||
+                         e->probe_class == KC_CHAIN);
   if (chain_on) KCK(hipMemsetAsync(b.chain[part], 0, (size_t)a.depth * 5 * b.chain_g4 * sizeof(unsigned), st));
   bool qkv_done = false;    // this layer's LayerNorm + QKV came with the previous layer's chain
   bool final_done = false;  // the final LayerNorm came with the last layer's chain
@@ -860,6 +861,7 @@ static int backbone_part(Ctx& c, int s0, int ns, hipStream_t st) {
       }
       ca.cnt = b.chain[part] + (size_t)l * 5 * b.chain_g4;
       ca.groups = (rows + kChainRows - 1) / kChainRows;
+      ProbeScope ps(e, KC_CHAIN, st, &c.site, &ca.probe);
       const hipError_t ce = chain_launch(bf, ca, st);
       if (ce == hipSuccess) {
         qkv_done = l + 1 < a.depth;

@@ -230,6 +230,7 @@ struct ChainDep {
   int wait_mult, wait_unit;  // a complete group holds wait_mult * ceil(rows of the group / wait_unit) arrivals
   unsigned* pub;         // this phase's row-group counters (null: last phase)
   unsigned* err;         // set to 1 when a wait gives up (bounded spin); the results are then garbage
+  unsigned long long* tl;  // (set per workgroup in the kernel) its timeline row when the launch is probed, or null
 };
 struct LnArgs {
   const void* h;  // [M, 1024] residual stream (operand dtype)
@@ -242,6 +243,8 @@ struct ChainArgs {
   LnArgs ln1, ln2;
   unsigned* cnt;   // [5][groups] arrival counters, zero before the launch
   int groups;      // ceil(M / kChainRows) (stride of cnt)
+  DevProbe probe;  // launch timing (f5h_probe_enable "chain"); timeline row per workgroup: entry, rows acquired,
+                   // results stored, exit
 };
 // bytes of cnt a chain launch over M rows uses (the caller zeroes them before every launch)
 inline size_t chain_counter_bytes(int M) {

@@ -58,7 +58,7 @@ EXPORTS = (
     "f5h_version",
 )
 
-KCLASS = {"ffn1": 0, "attention": 1, "qkv": 2, "ffn2": 3, "conv": 4, "out": 5, "norm": 6}
+KCLASS = {"ffn1": 0, "attention": 1, "qkv": 2, "ffn2": 3, "conv": 4, "out": 5, "norm": 6, "chain": 7}
 
 
 class Arch(ctypes.Structure):

@@ -180,7 +180,9 @@ int f5h_forward(f5h_engine* eng, void* stream, const f5h_forward_args* args, voi
  * get a stamp kernel on each side (no HIP events, so it also times graph replays; every 4th NFE
  * step is sampled). f5h_probe_read returns (sampled launches, total ms). Enabling resets the slots
  * and synchronises the device. Classes: 0 = FFN1 GEMM, 1 = attention, 2 = QKV GEMM, 3 = FFN2 GEMM,
- * 4 = conv, 5 = attention output-projection GEMM, 6 = pre-FFN norm (LayerNorm+modulate / RMSNorm). */
+ * 4 = conv, 5 = attention output-projection GEMM, 6 = pre-FFN norm (LayerNorm+modulate / RMSNorm), 7 = the phase
+ * chain launch (f5h_set_chain; its timeline row per workgroup: entry, rows acquired, results stored, exit). While
+ * one of the classes 0, 2, 3, 5, 6 is probed the chain is off (those launches are timed one by one). */
 int f5h_probe_enable(f5h_engine* eng, int32_t kclass, int32_t enable);
 int f5h_probe_read(f5h_engine* eng, int64_t* launches, double* total_ms);
 /* Per-workgroup timeline of the probed class's first launch in the first probed step (GEMM and
