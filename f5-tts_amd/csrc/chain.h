@@ -19,6 +19,10 @@ namespace f5h {
 
 constexpr int kAuxWT = 16;                 // buffer-store cache policy: sc1 (write-through)
 constexpr unsigned kChainSpinLimit = 1u << 18;
+// between polls: 16 x 64 clocks (~0.45 us). Waiting blocks poll while the previous phase computes on the same CUs,
+// and every poll sits in that CU's memory queue (MI355X_MICROARCH.md 'polling-cost'): with 2 x 64 clocks the
+// computing tiles of the chain ran 2-5 us longer than in their own launches (chain_timeline.py)
+constexpr int kChainSleep = 16;
 
 F5H_DEV void chain_wait(const ChainDep& d, int M, int r0, int nrows) {
   if (!d.wait) return;
@@ -38,7 +42,7 @@ F5H_DEV void chain_wait(const ChainDep& d, int M, int r0, int nrows) {
           __hip_atomic_store(d.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           break;
         }
-        __builtin_amdgcn_s_sleep(2);
+        __builtin_amdgcn_s_sleep(kChainSleep);
       }
     }
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
