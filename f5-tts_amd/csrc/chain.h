@@ -19,10 +19,10 @@ namespace f5h {
 
 constexpr int kAuxWT = 16;                 // buffer-store cache policy: sc1 (write-through)
 constexpr unsigned kChainSpinLimit = 1u << 18;
-// between polls: 16 x 64 clocks (~0.45 us). Waiting blocks poll while the previous phase computes on the same CUs,
-// and every poll sits in that CU's memory queue (MI355X_MICROARCH.md 'polling-cost'): with 2 x 64 clocks the
-// computing tiles of the chain ran 2-5 us longer than in their own launches (chain_timeline.py)
-constexpr int kChainSleep = 16;
+// between polls: 2 x 64 clocks (16 x 64, to take the pollers' loads out of the computing CUs' memory queues,
+// MI355X_MICROARCH.md 'polling-cost', left the computing tiles as slow and added latency to every hand-off:
+// profiles/r05_ab_c2_chain_tuning.txt)
+constexpr int kChainSleep = 2;
 
 F5H_DEV void chain_wait(const ChainDep& d, int M, int r0, int nrows) {
   if (!d.wait) return;

@@ -25,7 +25,7 @@ namespace f5h {
 namespace {
 
 // phase geometry: tile configs of the GEMM phases
-constexpr int kOutBM = 64, kFf1BM = 128, kFf2BM = 64, kQkvBM = 192, kBN = 128, kLnRows = 16;
+constexpr int kOutBM = 64, kFf1BM = 128, kFf2BM = 64, kQkvBM = 192, kBN = 128, kLnRows = 32;
 typedef GemmCfg<kOutBM, kBN, 2, 2, 3> CfgOut;
 typedef GemmCfg<kFf1BM, kBN, 2, 2, 2> CfgFf1;
 typedef GemmCfg<kQkvBM, kBN, 2, 2, 2> CfgQkv;
@@ -41,8 +41,9 @@ struct Launch {
   int start[7];  // first block of each phase (multiples of 8: a phase's block b and b + 8 share an XCD)
 };
 
-// LayerNorm phase: 16 rows per workgroup, 4 per wave, all four rows' loads in flight before the first reduction
-// (32-row units took 3.6-4.8 us each at C2: the LayerNorm phases set the chain's critical path, chain_timeline.py)
+// LayerNorm phase: 32 rows per workgroup, 8 per wave, all eight rows' loads in flight before the first reduction
+// (16-row units: 3.0 instead of 3.6 us per unit, but the phases ended later and C2 took 50.9 instead of 49.9 ms,
+// profiles/r05_ab_c2_chain_tuning.txt)
 template <typename T>
 F5H_DEV void ln_phase(const LnArgs& l, int M, int unit, const ChainDep& dep) {
   const int r0 = unit * kLnRows;

@@ -18,7 +18,7 @@ import bench  # noqa: E402
 from f5_tts_amd import parallel, synthetic  # noqa: E402
 
 
-def phase_starts(M, d=1024, ff=2048, nq=3072, qkv=True, ln_rows=16):
+def phase_starts(M, d=1024, ff=2048, nq=3072, qkv=True, ln_rows=32):
     cd = lambda a, b: (a + b - 1) // b
     r8 = lambda n: (n + 7) // 8 * 8
     cnt = [cd(M, 64) * (d // 128), cd(M, ln_rows), cd(M, 128) * (ff // 128), cd(M, 64) * (d // 128), cd(M, ln_rows),
