@@ -409,6 +409,11 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn16_kernel(AttnArgs a) {
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no LDS-DMA outlives the loop (ntile == 0 included)
   };
+  // the second-dispatched half (waves 4-7) at priority 1 for the whole loop: it otherwise loses VALU arbitration to
+  // the older half at the start of every segment (cdna_hip_programming.md T5, static form; the guard must be
+  // wave-uniform, or the scalar instruction runs for every wave). C2 49.08 vs 49.21 ms, attention 34.5 vs 34.7 us
+  // (profiles/r05_ab_c2_prio_split.txt)
+  if (__builtin_amdgcn_readfirstlane(threadIdx.x) >= 256) __builtin_amdgcn_s_setprio(1);
   pass(IF{});
   auto row_sum = [&]() -> float {
     if constexpr (RSM) return lacc[0];  // D[m][n] = sum_k P[n][k] for every m: lanes l and l + 32 alike

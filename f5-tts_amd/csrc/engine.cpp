@@ -788,7 +788,9 @@ static int backbone_part(Ctx& c, int s0, int ns, hipStream_t st) {
   // the final LayerNorm) as one launch. The 16-bit DiT path without row masks (single-utterance calls); not
   // while a chained class is probed (its launches are timed one by one).
   const int part = s0 ? 1 : 0;
-  const bool chain_on = dit && r16 && do_ln && e->chain && !keep && d == 1024 && b.chain[part] &&
+  // (one part only: two chain launches on the two CFG streams run 72 instead of 49 ms at C2, their waiting workgroups
+  // holding the slots the other stream's producers need, profiles/r05_ab_c2_prio_split.txt)
+  const bool chain_on = dit && r16 && do_ln && e->chain && !keep && d == 1024 && b.chain[part] && ns == c.S &&
                         (e->probe_class < 0 || e->probe_class == KC_ATTN || e->probe_class == KC_CONV ||
                          e->probe_class == KC_CHAIN);
   if (chain_on) KCK(hipMemsetAsync(b.chain[part], 0, (size_t)a.depth * 5 * b.chain_g4 * sizeof(unsigned), st));
