@@ -1,5 +1,6 @@
 """Summarise a tools/gpu_vendor.sh run into profiles/<name>.json: per op the hipBLASLt / SDPA kernel-trace average
-(timed launches only: the first 3 of each op's dispatch run are its warm-up) and the HIP-event average.
+(timed launches only: the first 3 of each op's dispatch run are its warm-up) and the HIP-event average,
+plus this build's per-class kernel-trace averages from the same box ("ours", when the run traced them).
 
   python tools/vendor_summary.py gpurun_out/<dir> profiles/r05_vendor_c2_c4.json
 """
@@ -42,5 +43,13 @@ for k in ("c2_attention", "c4_attention"):
         o = {kk: v for kk, v in ev["ops"][k].items() if kk not in ("us", "frac", "tflops")}
         o["event_us"] = round(ev["ops"][k]["us"], 2)
         res["ops"][k] = o
+# this build's per-class kernel-trace averages from the same box (gpu_vendor.sh traces them after the vendor run)
+for cfg in ("c2", "c4"):
+    f = os.path.join(d, f"classes_{cfg}.json")
+    if os.path.exists(f):
+        j = json.load(open(f))
+        res.setdefault("ours", {})[cfg] = {"head": j.get("head"), "src_hash": j.get("src_hash"),
+                                           "classes": {c: {"avg_launch_us": v["avg_launch_us"]}
+                                                       for c, v in j["classes"].items()}}
 json.dump(res, open(out, "w"), indent=1)
 print(json.dumps(res["ops"], indent=1))

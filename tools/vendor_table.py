@@ -1,15 +1,15 @@
 """Markdown table of this build's per-class kernel-trace averages against the vendor libraries on the same box
 (VERDICT r04 item 4): hipBLASLt GEMMs (torch.mm, no epilogue) and torch SDPA at the C2 and C4-per-rank shapes.
 
-  python tools/vendor_table.py profiles/r05_vendor_c2_c4.json profiles/r05_rocprof_classes_c2.json \
-      profiles/r05_rocprof_classes_c4.json
+  python tools/vendor_table.py profiles/r05_vendor_c2_c4.json [profiles/r05_rocprof_classes_c2.json ...]
 """
 import json
 import sys
 
-vendor = json.load(open(sys.argv[1]))["ops"]
-ours = {}
-for path in sys.argv[2:]:
+vj = json.load(open(sys.argv[1]))
+vendor = vj["ops"]
+ours = {cfg: o["classes"] for cfg, o in vj.get("ours", {}).items()}  # same box as the vendor run
+for path in sys.argv[2:]:  # or per-class summaries given explicitly (these win)
     j = json.load(open(path))
     cfg = "c2" if j["shape"].get("S") == 2 else "c4"
     ours[cfg] = j["classes"]
