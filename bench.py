@@ -259,11 +259,14 @@ def cpu_baseline(config, case, arch, threads):
 
 
 def class_flops(kc, arch, S, L):
-    """Algorithmic FLOPs of one launch of a probed kernel class (SURVEY §8d per-op terms)."""
+    """Algorithmic FLOPs of one launch of a probed kernel class (SURVEY §8d per-op terms). The phase chain (C2's
+    shipped form: one launch per layer running out-proj, LayerNorm, FFN1, FFN2, the next layer's LayerNorm and its
+    QKV) is priced on its GEMM phases, averaged over the depth launches of a step (the last layer's has no QKV)."""
     d, ff = arch["dim"], int(arch["dim"] * arch["ff_mult"])
+    chain = 2.0 * S * L * d * (d + 2 * ff) + 2.0 * S * L * d * 3 * d * (arch["depth"] - 1) / arch["depth"]
     return {"attention": attn_flops(S, arch["heads"], L), "ffn1": 2.0 * S * L * d * ff, "ffn2": 2.0 * S * L * d * ff,
             "qkv": 2.0 * S * L * d * 3 * d, "out": 2.0 * S * L * d * d,
-            "conv": 2.0 * S * L * d * (d // 16) * 31}.get(kc, 0.0)
+            "conv": 2.0 * S * L * d * (d // 16) * 31, "chain": chain}.get(kc, 0.0)
 
 
 def resid_bytes(arch, esz=2):
@@ -282,7 +285,10 @@ def class_bytes(kc, arch, S, L, esz=2):
     return 0.0
 
 
-PROBE_CLASSES = ("qkv", "attention", "out", "norm", "ffn1", "ffn2", "conv")
+# "chain": the phase-chain launch (16-bit DiT calls without row masks, i.e. C2): while one of qkv/out/norm/ffn1/ffn2
+# is probed the chain is off (those launches are timed one by one), so their rows describe the unchained form and
+# the chain row the form C2 ships; the chain probe times nothing at the other configs (no launch: no row)
+PROBE_CLASSES = ("qkv", "attention", "out", "norm", "ffn1", "ffn2", "conv", "chain")
 PEAK_HBM_GBPS = 8000.0
 
 
@@ -643,6 +649,7 @@ def run_rank(args):
     for kc in ("qkv", "attention", "out", "ffn1", "ffn2"):
         launches[kc] = arch["depth"]
     launches["conv"] = 1
+    launches["chain"] = arch["depth"]
     # the pad-row skip runs on the batch path (B > 1, one bucket): attention and out-proj work on live rows
     qlens = None
     if B > 1 and len(batches) == 1 and os.environ.get("F5H_NO_PAD_SKIP") != "1":

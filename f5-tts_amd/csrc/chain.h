@@ -6,11 +6,13 @@
 //     row group its tile covers;
 //   consumer workgroup: ONE wave polls each needed counter (relaxed agent loads + s_sleep, bounded) -> ONE
 //     agent-scope acquire (drops this CU's L1) -> s_waitcnt vmcnt(0) -> __syncthreads() -> plain loads.
-// Counters are zeroed by a memset node ahead of every launch (Guideline 16, 'Re-initialise every call').
+// Counters are zeroed by one memset node per step (Guideline 16, 'Re-initialise every call'): each layer's launch
+// has its own [5][groups] block of them.
 // Progress: a phase's workgroups have higher ids than every producer they wait for, and the dispatcher hands
 // out ids in order on each XCD, so every producer is resident or finished before any consumer can wait on it
 // (a waiting block never keeps a producer from being dispatched). The bounded spin only guards against a bug:
-// it gives up after ~0.3 s, sets the fault word and lets the launch drain (chain_fault_take reads it).
+// it gives up after ~0.3 s, sets the ENGINE's fault word (ChainDep::err, engine-owned device memory) and lets the
+// launch drain; the call's final kernel then writes NaN results, and the engine's next call fails (engine.cpp).
 #pragma once
 #include "common.h"
 #include "kernels.h"
@@ -38,7 +40,7 @@ F5H_DEV void chain_wait(const ChainDep& d, int M, int r0, int nrows) {
         const unsigned v =
             __builtin_amdgcn_readfirstlane(__hip_atomic_load(d.wait + gi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
         if (v >= need) break;
-        if (spins > kChainSpinLimit) {
+        if (spins >= d.spin_limit) {
           __hip_atomic_store(d.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           break;
         }

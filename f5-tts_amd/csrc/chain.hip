@@ -18,6 +18,7 @@
 #include "gemm_impl.h"
 #include "lnrow.h"
 
+#include <algorithm>
 #include <atomic>
 
 namespace f5h {
@@ -32,8 +33,7 @@ typedef GemmCfg<kQkvBM, kBN, 2, 2, 2> CfgQkv;
 constexpr int cmax(int a, int b) { return a > b ? a : b; }
 constexpr int kLdsBytes = cmax(cmax(CfgOut::bytes, CfgFf1::bytes), CfgQkv::bytes);
 
-__device__ unsigned g_chain_fault;  // the bounded waits' give-up word (ChainDep::err)
-std::atomic<int64_t> g_launches{0};
+std::atomic<long long> g_spin_limit{(long long)kChainSpinLimit};  // test hook: chain_set_spin_limit
 
 struct Launch {
   ChainArgs a;
@@ -143,18 +143,16 @@ hipError_t chain_launch(int compute, const ChainArgs& a, hipStream_t st) {
   const int cnt[6] = {n_out, n_ln, n_ff1, n_ff2, n_ln, n_qkv};
   L.start[0] = 0;
   for (int p = 0; p < 6; ++p) L.start[p + 1] = L.start[p] + round8(cnt[p]);
-  static unsigned* err = [] {  // resolved once (not inside a stream capture)
-    void* p = nullptr;
-    return hipGetSymbolAddress(&p, HIP_SYMBOL(g_chain_fault)) == hipSuccess ? static_cast<unsigned*>(p) : nullptr;
-  }();
-  if (!err) return hipErrorInvalidValue;
+  if (!a.fault) return hipErrorInvalidValue;
+  const unsigned spin_limit = (unsigned)g_spin_limit.load(std::memory_order_relaxed);
   // producers' arrivals per complete row group: a GEMM tile adds 1 to each group it covers (its row block
   // spans whole groups), so a group is complete at (column tiles) arrivals; a LayerNorm unit covers half a group
   const int mult[6] = {d / kBN, 1, ff / kBN, d / kBN, 1, 0};
   const int unit[6] = {kChainRows, kLnRows, kChainRows, kChainRows, kLnRows, 0};
   for (int p = 0; p < 6; ++p) {
     ChainDep& x = L.dep[p];
-    x.err = err;
+    x.err = a.fault;
+    x.spin_limit = spin_limit;
     x.pub = p < 5 ? a.cnt + (size_t)p * a.groups : nullptr;
     x.wait = p > 0 ? a.cnt + (size_t)(p - 1) * a.groups : nullptr;
     x.wait_mult = p > 0 ? mult[p - 1] : 0;
@@ -165,18 +163,12 @@ hipError_t chain_launch(int compute, const ChainArgs& a, hipStream_t st) {
     hipLaunchKernelGGL(chain_kernel<bf16>, grid, block, 0, st, L);
   else
     hipLaunchKernelGGL(chain_kernel<f16>, grid, block, 0, st, L);
-  const hipError_t e = hipGetLastError();
-  if (e == hipSuccess) g_launches.fetch_add(1, std::memory_order_relaxed);
-  return e;
+  return hipGetLastError();
 }
 
-int64_t chain_launches() { return g_launches.load(std::memory_order_relaxed); }
-
-int chain_fault_take() {
-  unsigned v = 0, z = 0;
-  if (hipMemcpyFromSymbol(&v, HIP_SYMBOL(g_chain_fault), sizeof(v)) != hipSuccess) return -1;
-  if (v) (void)hipMemcpyToSymbol(HIP_SYMBOL(g_chain_fault), &z, sizeof(z));
-  return (int)v;
+void chain_set_spin_limit(long long limit) {
+  g_spin_limit.store(limit < 0 ? (long long)kChainSpinLimit : std::min<long long>(limit, 0xffffffffll),
+                     std::memory_order_relaxed);
 }
 
 }  // namespace f5h

@@ -596,18 +596,20 @@ hipError_t final_where(const float* cond, const uint8_t* cond_mask, float* y, in
   hipLaunchKernelGGL(final_where_kernel, dim3(nblk(total, 256)), dim3(256), 0, st, cond, cond_mask, y, total, mel);
   return hipGetLastError();
 }
-// out = where(cond_mask, cond, y) from the workspace ODE state y
+// out = where(cond_mask, cond, y) from the workspace ODE state y. fault (or null): the engine's phase-chain give-up
+// word; when a bounded wait of this call's chain launches expired, the results are wrong and out is NaN instead
 __global__ void final_where_out_kernel(const float* cond, const uint8_t* m, const float* y, float* out,
-                                       int64_t total, int mel) {
+                                       int64_t total, int mel, const unsigned* fault) {
   int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= total) return;
-  out[i] = m[i / mel] ? cond[i] : y[i];
+  const bool bad = fault && __builtin_nontemporal_load(fault) != 0u;
+  out[i] = bad ? __builtin_nanf("") : (m[i / mel] ? cond[i] : y[i]);
 }
 hipError_t final_where_out(const float* cond, const uint8_t* cond_mask, const float* y, float* out, int B, int N,
-                           int mel, hipStream_t st) {
+                           int mel, const unsigned* fault, hipStream_t st) {
   const int64_t total = (int64_t)B * N * mel;
   hipLaunchKernelGGL(final_where_out_kernel, dim3(nblk(total, 256)), dim3(256), 0, st, cond, cond_mask, y, out,
-                     total, mel);
+                     total, mel, fault);
   return hipGetLastError();
 }
 
@@ -651,18 +653,22 @@ hipError_t write_time_token(int compute, int h16, const float* temb, int S, int 
   return hipGetLastError();
 }
 
-__global__ void copy_pred_kernel(const float* p, int S, int L, int off, int mel, int64_t ld, float* dst) {
+__global__ void copy_pred_kernel(const float* p, int S, int L, int off, int mel, int64_t ld, float* dst,
+                                 const unsigned* fault) {
   const int Lo = L - off;
   int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= (int64_t)S * Lo * mel) return;
   int c = (int)(i % mel);
   int64_t r = i / mel;
   int s = (int)(r / Lo), n = (int)(r - (int64_t)s * Lo);
-  dst[i] = p[((int64_t)s * L + off + n) * ld + c];
+  const bool bad = fault && __builtin_nontemporal_load(fault) != 0u;  // as final_where_out
+  dst[i] = bad ? __builtin_nanf("") : p[((int64_t)s * L + off + n) * ld + c];
 }
-hipError_t copy_pred(const float* p, int S, int L, int row_off, int mel, int64_t p_ld, float* dst, hipStream_t st) {
+hipError_t copy_pred(const float* p, int S, int L, int row_off, int mel, int64_t p_ld, float* dst,
+                     const unsigned* fault, hipStream_t st) {
   const int64_t total = (int64_t)S * (L - row_off) * mel;
-  hipLaunchKernelGGL(copy_pred_kernel, dim3(nblk(total, 256)), dim3(256), 0, st, p, S, L, row_off, mel, p_ld, dst);
+  hipLaunchKernelGGL(copy_pred_kernel, dim3(nblk(total, 256)), dim3(256), 0, st, p, S, L, row_off, mel, p_ld, dst,
+                     fault);
   return hipGetLastError();
 }
 

@@ -107,6 +107,8 @@ struct f5h_engine {
   // new shape runs it eagerly instead of paying capture + instantiate for one replay)
   std::vector<struct GraphKey> pro_seen;
   int64_t n_evicted = 0, n_reaped = 0;
+  std::mutex hm;
+  double last_host[8] = {};  // f5h_last_call_host_ms: the newest f5h_sample call's host phases
   hipStream_t cap = nullptr;  // private capture stream (the caller's may be the null stream)
   hipStream_t cap2 = nullptr; // second capture stream: the unconditional CFG branch
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;
@@ -121,6 +123,13 @@ struct f5h_engine {
   // In-launch phase chain of the DiT block-step's row-local seams (chain.hip): f5h_set_chain, env F5H_CHAIN=0 at
   // creation turns it off. Bitwise identical results.
   int chain = 1;
+  // The chain's give-up word (chain.h): device memory of the engine, set by a chain wait that expired. The call's final
+  // kernel then writes NaN results; a copy of it lands in a pinned host word (fault_host) at the end of every chained
+  // call, and the engine's next call reads that word, fails with F5H_EHIP and switches the chain off.
+  unsigned* chain_fault = nullptr;
+  volatile unsigned* fault_host = nullptr;
+  int fault_slot = -1;
+  std::atomic<int64_t> n_chain{0};  // chain launches enqueued (eager launches and captures)
   uint64_t use_ctr = 0;
   int64_t n_captures = 0, n_replays = 0;
   // probe
@@ -467,7 +476,7 @@ struct Bufs {
   float2* rope;
   uint8_t* rowkeep;
   int32_t* kvlen;
-  unsigned* chain[2];  // phase-chain arrival counters per CFG part: [depth][5][chain_g4]
+  unsigned* chain;     // phase-chain arrival counters: [depth][5][chain_g4] (the chain runs on the packed batch only)
   int chain_g4;        // row groups per counter row, rounded up to 4 (16-B rows)
   float *ada_cur, *temb_cur, *tgrid;  // the current step's table rows; device copy of the grid
   int* kstep;                         // device-side NFE step index
@@ -524,8 +533,7 @@ static void layout(const f5h_engine* e, WS& ws, Bufs& b, int B, int N, int nfe, 
   b.rowkeep = ws.take<uint8_t>(rows);
   b.kvlen = ws.take<int32_t>(S);
   b.chain_g4 = ((int)((rows + kChainRows - 1) / kChainRows) + 3) / 4 * 4;
-  for (int p = 0; p < 2; ++p)
-    b.chain[p] = a.backbone == F5H_DIT ? ws.take<unsigned>((size_t)a.depth * 5 * b.chain_g4) : nullptr;
+  b.chain = a.backbone == F5H_DIT ? ws.take<unsigned>((size_t)a.depth * 5 * b.chain_g4) : nullptr;
   b.ada_cur = a.backbone == F5H_DIT ? ws.take<float>((size_t)e->ada.Npad) : nullptr;
   b.temb_cur = ws.take<float>((size_t)d);
   b.tgrid = ws.take<float>((size_t)nfe);
@@ -583,7 +591,14 @@ struct Ctx {
   int drop_audio, drop_text;  // single-branch forward only (f5h_forward with cfg_infer = 0)
   hipStream_t st2;            // second stream for the unconditional branch (step-graph capture), or null
   int site;  // probe launch-site counter, reset at the start of every step's enqueue
+  int chain;  // this call may run the phase chain (engine switch, shape, and chain_admit's per-device check)
+  double* hp;  // host milliseconds of the call by phase (kHostPhases, f5h_last_call_host_ms), or null
 };
+// Host time of an f5h_sample call by phase (f5h_last_call_host_ms): a call that blocks the host shows where.
+enum { HP_TOTAL = 0, HP_PROLOGUE, HP_LOCK, HP_REAP, HP_CAPTURE, HP_INSTANTIATE, HP_LAUNCH, HP_FINAL, kHostPhases };
+static double host_ms() {
+  return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
 
 static GemmArgs gargs(const void* A, int64_t lda, const Lin& W, int M, void* C, int64_t ldc) {
   GemmArgs g{};
@@ -787,13 +802,13 @@ static int backbone_part(Ctx& c, int s0, int ns, hipStream_t st) {
   // In-launch phase chain (chain.hip): a layer's out-proj .. FFN2 plus the next layer's LayerNorm + QKV (or
   // the final LayerNorm) as one launch. The 16-bit DiT path without row masks (single-utterance calls); not
   // while a chained class is probed (its launches are timed one by one).
-  const int part = s0 ? 1 : 0;
-  // (one part only: two chain launches on the two CFG streams run 72 instead of 49 ms at C2, their waiting workgroups
-  // holding the slots the other stream's producers need, profiles/r05_ab_c2_prio_split.txt)
-  const bool chain_on = dit && r16 && do_ln && e->chain && !keep && d == 1024 && b.chain[part] && ns == c.S &&
+  // (the packed batch only, s0 == 0: two chain launches on the two CFG streams run 72 instead of 49 ms at C2, their
+  // waiting workgroups holding the slots the other stream's producers need, profiles/r05_ab_c2_prio_split.txt; for
+  // the same reason c.chain is off while another stream's chained call is in flight, chain_admit)
+  const bool chain_on = c.chain && dit && r16 && do_ln && !keep && d == 1024 && b.chain && s0 == 0 && ns == c.S &&
                         (e->probe_class < 0 || e->probe_class == KC_ATTN || e->probe_class == KC_CONV ||
                          e->probe_class == KC_CHAIN);
-  if (chain_on) KCK(hipMemsetAsync(b.chain[part], 0, (size_t)a.depth * 5 * b.chain_g4 * sizeof(unsigned), st));
+  if (chain_on) KCK(hipMemsetAsync(b.chain, 0, (size_t)a.depth * 5 * b.chain_g4 * sizeof(unsigned), st));
   bool qkv_done = false;    // this layer's LayerNorm + QKV came with the previous layer's chain
   bool final_done = false;  // the final LayerNorm came with the last layer's chain
   for (int l = 0; l < a.depth; ++l) {
@@ -861,11 +876,13 @@ static int backbone_part(Ctx& c, int s0, int ns, hipStream_t st) {
         const float* fin = ada_k + (size_t)a.depth * 6 * d;  // AdaLayerNorm_Final: (scale, shift)
         ca.ln2 = LnArgs{h, aop, fin + d, fin};
       }
-      ca.cnt = b.chain[part] + (size_t)l * 5 * b.chain_g4;
+      ca.cnt = b.chain + (size_t)l * 5 * b.chain_g4;
       ca.groups = (rows + kChainRows - 1) / kChainRows;
+      ca.fault = e->chain_fault;
       ProbeScope ps(e, KC_CHAIN, st, &c.site, &ca.probe);
       const hipError_t ce = chain_launch(bf, ca, st);
       if (ce == hipSuccess) {
+        e->n_chain.fetch_add(1, std::memory_order_relaxed);
         qkv_done = l + 1 < a.depth;
         final_done = l + 1 == a.depth;
         continue;
@@ -934,6 +951,134 @@ static int backbone_step(Ctx& c) {
   RC(backbone_part(c, c.B, c.B, c.st2));
   KCK(hipEventRecord(e->ev_join, c.st2));
   KCK(hipStreamWaitEvent(c.st, e->ev_join, 0));
+  return 0;
+}
+
+// ---------------------------------------------------------------- phase-chain admission and fault word
+// Pinned host words the engines' fault copies land in: one slab per process (allocated once; a hipHostFree per engine
+// could wait for the device), slots handed out and returned by index.
+static std::mutex g_slot_m;
+static unsigned* g_slots = nullptr;
+static std::vector<int> g_free_slots;
+static constexpr int kFaultSlots = 4096;
+static int fault_slot_take(volatile unsigned** host) {
+  std::lock_guard<std::mutex> lk(g_slot_m);
+  if (!g_slots) {
+    void* p = nullptr;
+    if (hipHostMalloc(&p, kFaultSlots * 64, hipHostMallocDefault) != hipSuccess) return -1;
+    g_slots = static_cast<unsigned*>(p);
+    for (int i = kFaultSlots - 1; i >= 0; --i) g_free_slots.push_back(i);
+  }
+  if (g_free_slots.empty()) return -1;
+  const int i = g_free_slots.back();
+  g_free_slots.pop_back();
+  *host = g_slots + (size_t)i * 16;  // one 64-B line per slot
+  **host = 0u;
+  return i;
+}
+static void fault_slot_give(int i) {
+  if (i < 0) return;
+  std::lock_guard<std::mutex> lk(g_slot_m);
+  g_free_slots.push_back(i);
+}
+
+// Per-device admission of chained calls. Two phase-chain launches in flight at once starve each
+// other: each one's waiting workgroups hold CU slots the other's producers need (C2 72 instead of 49 ms with the two
+// CFG branches on their own streams, profiles/r05_ab_c2_prio_split.txt). A call that would chain while a chained
+// call from ANOTHER stream is still being enqueued or still runs on the device (its "done" event not complete) takes
+// the separate launches instead (bitwise identical results). Calls on one stream are ordered by the stream itself.
+// Non-blocking: one hipEventQuery, no wait.
+struct ChainGate {
+  std::mutex m;
+  hipStream_t owner = nullptr;
+  bool owned = false;
+  int enqueuing = 0;          // chained calls of the owner stream being enqueued
+  hipEvent_t done = nullptr;  // recorded on the owner stream after its last chained call
+  bool pending = false;
+};
+static ChainGate g_gate[64];
+static std::atomic<int64_t> g_gate_refused{0};
+
+static bool chain_admit(int dev, hipStream_t st) {
+  ChainGate& g = g_gate[dev & 63];
+  std::lock_guard<std::mutex> lk(g.m);
+  if (g.owned && g.owner != st) {
+    bool busy = g.enqueuing > 0;
+    if (!busy && g.pending) {
+      busy = hipEventQuery(g.done) == hipErrorNotReady;
+      (void)hipGetLastError();  // hipErrorNotReady is the expected answer for a pending event
+      if (!busy) g.pending = false;
+    }
+    if (busy) {
+      g_gate_refused.fetch_add(1, std::memory_order_relaxed);
+      return false;
+    }
+  }
+  g.owner = st;
+  g.owned = true;
+  ++g.enqueuing;
+  return true;
+}
+static void chain_leave(int dev, hipStream_t st) {
+  ChainGate& g = g_gate[dev & 63];
+  std::lock_guard<std::mutex> lk(g.m);
+  --g.enqueuing;
+  if (!g.done && hipEventCreateWithFlags(&g.done, hipEventDisableTiming) != hipSuccess) {
+    (void)hipGetLastError();
+    g.done = nullptr;
+    return;
+  }
+  if (hipEventRecord(g.done, st) == hipSuccess)
+    g.pending = true;
+  else
+    (void)hipGetLastError();
+}
+// Held for one call: admits the call's chain (or not) and, on every return path, records the gate's "done" event
+// after the call's launches.
+struct ChainTicket {
+  int dev = 0;
+  hipStream_t st = nullptr;
+  bool held = false;
+  ~ChainTicket() {
+    if (held) chain_leave(dev, st);
+  }
+};
+// Could this call's step run the chain? (the engine switch and the shapes backbone_part checks per part); if so,
+// ask the gate.
+static int chain_for_call(f5h_engine* e, const Ctx& c, ChainTicket& t) {
+  static const bool res32 = [] {
+    const char* v = getenv("F5H_RES32");
+    return v && *v == '1';
+  }();
+  const bool split = e->graph_mode && e->split_cfg == 1 && c.use_cfg;  // the two CFG parts: no chain
+  if (!e->chain || e->a.backbone != F5H_DIT || e->bf == 0 || res32 || e->a.dim != 1024 || c.batch_mask || split ||
+      !e->chain_fault)
+    return 0;
+  if (!chain_admit(e->dev, c.st)) return 0;
+  t.dev = e->dev;
+  t.st = c.st;
+  t.held = true;
+  return 1;
+}
+// Start of every sample/forward call: a give-up recorded by an earlier chained call of this engine (its copy in the
+// pinned word, landed once that call completed) fails this call and switches the chain off for the engine.
+static int chain_fault_check(f5h_engine* e, hipStream_t st) {
+  if (!e->fault_host || *e->fault_host == 0u) return 0;
+  *e->fault_host = 0u;
+  {
+    std::lock_guard<std::mutex> g(e->gm);
+    e->chain = 0;
+  }
+  (void)hipMemsetAsync(e->chain_fault, 0, sizeof(unsigned), st);
+  return fail(F5H_EHIP,
+              "phase chain: a wait for a producer row group gave up in an earlier call of this engine (its output was "
+              "set to NaN); the chain is now off for this engine (f5h_set_chain re-enables it)");
+}
+// End of a chained call: the fault word's copy to the pinned host word, stream-ordered behind the call
+static int chain_fault_note(f5h_engine* e, hipStream_t st) {
+  if (!e->fault_host) return 0;
+  HIPCK(hipMemcpyAsync(const_cast<unsigned*>(e->fault_host), e->chain_fault, sizeof(unsigned), hipMemcpyDeviceToHost,
+                       st));
   return 0;
 }
 
@@ -1049,6 +1194,17 @@ int f5h_engine_create_views(const f5h_arch* arch, const f5h_tensor_view* weights
       f5h_engine_destroy(e);
       return fail(F5H_EHIP, "probe buffers");
     }
+    void* fw = nullptr;
+    if (dalloc(e, 64, &fw) || hipStreamSynchronize(e->mstream) != hipSuccess) {
+      f5h_engine_destroy(e);
+      return fail(F5H_EHIP, "chain fault word");
+    }
+    e->chain_fault = reinterpret_cast<unsigned*>(fw);
+    e->fault_slot = fault_slot_take(&e->fault_host);
+    if (e->fault_slot < 0) {  // no pinned word: the chain stays off (its give-ups could not be reported)
+      (void)hipGetLastError();
+      e->chain_fault = nullptr;
+    }
     e->pstamp = reinterpret_cast<unsigned long long*>(p);
     e->pslots = e->pstamp + 64;
     e->ptick = reinterpret_cast<int*>(e->pstamp);
@@ -1097,6 +1253,7 @@ void f5h_engine_destroy(f5h_engine* e) {
     // stream-ordered releases into the pool: no device-wide wait (hipFree would wait for every stream)
     for (void* p : e->allocs) dev_free(p, e->mstream);
     if (e->mstream) (void)hipStreamDestroy(e->mstream);
+    fault_slot_give(e->fault_slot);  // after the use events: the last fault copy has landed
     delete e;
   });
 }
@@ -1181,6 +1338,12 @@ int f5h_sample(f5h_engine* e, void* stream, const f5h_sample_args* a, void* work
   c.L = e->a.backbone == F5H_DIT ? c.N : c.N + 1;
   c.batch_mask = a->use_batch_mask ? 1 : 0;
   RC(check_ws(e, c.B, c.N, c.nfe, c.use_cfg, workspace, workspace_bytes, c));
+  RC(chain_fault_check(e, c.st));
+  ChainTicket ticket;  // (declared after `used`: its event is recorded first, both after every launch of the call)
+  c.chain = chain_for_call(e, c, ticket);
+  double hp[kHostPhases] = {};
+  c.hp = hp;
+  const double h0 = host_ms();
   static const bool pro_graph = [] {
     const char* v = getenv("F5H_PROLOGUE_GRAPH");
     return !(v && *v == '0');
@@ -1192,6 +1355,7 @@ int f5h_sample(f5h_engine* e, void* stream, const f5h_sample_args* a, void* work
     RC(prologue_graph(c, a, pkey));
   else
     RC(prologue(c, a->t_grid, c.nfe, a->cond, a->cond_mask, a->text, a->duration));
+  const double h1 = host_ms();
   const size_t ysz = (size_t)c.B * c.N * e->a.mel_dim;
   HIPCK(hipMemcpyAsync(c.b.y, a->y0, ysz * sizeof(float), hipMemcpyDeviceToDevice, c.st));
   if (a->trajectory)
@@ -1202,8 +1366,22 @@ int f5h_sample(f5h_engine* e, void* stream, const f5h_sample_args* a, void* work
   // is copied here, every later one by the previous step's Euler launch
   HIPCK(hipMemsetAsync(c.b.kstep, 0, 64 * sizeof(int), c.st));
   RC(step_prep(c));
+  const double h2 = host_ms();
+  const double g2 = hp[HP_LOCK] + hp[HP_REAP] + hp[HP_CAPTURE] + hp[HP_INSTANTIATE];
   RC(run_steps(c, a, workspace));
-  HIPCK(final_where_out(a->cond, a->cond_mask, c.b.y, a->out, c.B, c.N, e->a.mel_dim, c.st));
+  const double h3 = host_ms();
+  HIPCK(final_where_out(a->cond, a->cond_mask, c.b.y, a->out, c.B, c.N, e->a.mel_dim,
+                        c.chain ? e->chain_fault : nullptr, c.st));
+  if (c.chain) RC(chain_fault_note(e, c.st));
+  const double h4 = host_ms();
+  hp[HP_TOTAL] = h4 - h0;
+  hp[HP_PROLOGUE] = h1 - h0;
+  hp[HP_LAUNCH] = (h3 - h2) - (hp[HP_LOCK] + hp[HP_REAP] + hp[HP_CAPTURE] + hp[HP_INSTANTIATE] - g2);
+  hp[HP_FINAL] = h4 - h3;
+  {
+    std::lock_guard<std::mutex> g(e->hm);
+    std::memcpy(e->last_host, hp, sizeof(hp));
+  }
   return 0;
 }
 
@@ -1264,7 +1442,7 @@ static int run_steps(Ctx& c, const f5h_sample_args* a, const void* ws) {
   const bool split = e->split_cfg == 1;  // auto (2): one packed chain
   key.split = split;
   key.pad_skip = e->pad_skip;
-  key.chain = e->chain;
+  key.chain = c.chain;
   key.kernel_epoch = g_kernel_epoch.load();
   std::memcpy(&key.cfg_bits, &a->cfg_strength, 4);
   std::shared_ptr<GraphEntry> hold;  // keeps the replayed graph alive through the launch loop
@@ -1294,10 +1472,6 @@ static bool host_trace() {
   }();
   return on;
 }
-static double host_ms() {
-  return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
-}
-
 // Destroy graveyard entries that nothing replays any more: every event recorded after their
 // replays has completed and no caller holds them. Non-blocking (hipEventQuery); caller holds e->gm.
 static void reap_graphs(f5h_engine* e) {
@@ -1351,12 +1525,16 @@ static int note_replays(f5h_engine* e, GraphEntry* g, hipStream_t st) {
 static int graph_get(Ctx& c, const GraphKey& key, bool split, const std::function<int(Ctx&)>& body,
                      std::shared_ptr<GraphEntry>& hold, int64_t replays) {
   f5h_engine* e = c.e;
-  const double t0 = host_trace() ? host_ms() : 0.0;
+  const double t0 = host_ms();
   std::lock_guard<std::mutex> g(e->gm);
-  const double t1 = host_trace() ? host_ms() : 0.0;
+  const double t1 = host_ms();
   const int64_t reaped0 = e->n_reaped;
   reap_graphs(e);
-  const double t2 = host_trace() ? host_ms() : 0.0;
+  const double t2 = host_ms();
+  if (c.hp) {
+    c.hp[HP_LOCK] += t1 - t0;
+    c.hp[HP_REAP] += t2 - t1;
+  }
   if (host_trace())
     std::fprintf(stderr, "[f5h host] graph_get kind %d: lock %.3f ms, reap %.3f ms (%lld destroyed)\n", key.kind,
                  t1 - t0, t2 - t1, (long long)(e->n_reaped - reaped0));
@@ -1374,7 +1552,7 @@ static int graph_get(Ctx& c, const GraphKey& key, bool split, const std::functio
     Ctx cc = c;
     cc.st = e->cap;
     cc.st2 = split ? e->cap2 : nullptr;
-    const double c0 = host_trace() ? host_ms() : 0.0;
+    const double c0 = host_ms();
     hipError_t be = hipStreamBeginCapture(e->cap, hipStreamCaptureModeThreadLocal);
     if (be != hipSuccess) return fail(F5H_EHIP, std::string("hipStreamBeginCapture: ") + hipGetErrorString(be));
     const int rc = body(cc);
@@ -1385,9 +1563,13 @@ static int graph_get(Ctx& c, const GraphKey& key, bool split, const std::functio
       if (rc) return rc;
       return fail(F5H_EHIP, std::string("hipStreamEndCapture: ") + hipGetErrorString(ce));
     }
-    const double c1 = host_trace() ? host_ms() : 0.0;
+    const double c1 = host_ms();
     const hipError_t ie = hipGraphInstantiate(&ne->exec, graph, nullptr, nullptr, 0);
     (void)hipGraphDestroy(graph);
+    if (c.hp) {
+      c.hp[HP_CAPTURE] += c1 - c0;
+      c.hp[HP_INSTANTIATE] += host_ms() - c1;
+    }
     if (host_trace())
       std::fprintf(stderr, "[f5h host] capture %.3f ms, instantiate %.3f ms\n", c1 - c0, host_ms() - c1);
     if (ie != hipSuccess) {
@@ -1447,6 +1629,9 @@ int f5h_forward(f5h_engine* e, void* stream, const f5h_forward_args* a, void* wo
   if (e->a.backbone == F5H_DIT && a->N > 8192) return fail(F5H_EINVAL, "N exceeds the text position table (8192)");
   if (a->text_cache < 0 || a->text_cache > 2) return fail(F5H_EINVAL, "text_cache must be 0, 1 or 2");
   RC(check_ws(e, c.B, c.N, 1, c.use_cfg, workspace, workspace_bytes, c));
+  RC(chain_fault_check(e, c.st));
+  ChainTicket ticket;
+  c.chain = chain_for_call(e, c, ticket);
   const bool cached = a->text_cache == 2;
   if (a->t_dev) {  // time read on the stream: no host round trip (dit.py:332-333 takes a tensor)
     HIPCK(hipMemcpyAsync(c.b.tgrid, a->t_dev, sizeof(float), hipMemcpyDeviceToDevice, c.st));
@@ -1478,7 +1663,7 @@ int f5h_forward(f5h_engine* e, void* stream, const f5h_forward_args* a, void* wo
     key.batch_mask = c.batch_mask;
     key.probe = e->probe_class;
     key.pad_skip = e->pad_skip;
-    key.chain = e->chain;
+    key.chain = c.chain;
     key.kernel_epoch = g_kernel_epoch.load();
     std::shared_ptr<GraphEntry> hold;
     RC(graph_get(c, key, false, body, hold, 1));
@@ -1487,7 +1672,9 @@ int f5h_forward(f5h_engine* e, void* stream, const f5h_forward_args* a, void* wo
   } else {
     RC(body(c));
   }
-  HIPCK(copy_pred(c.b.p, c.S, c.L, e->a.backbone == F5H_DIT ? 0 : 1, e->a.mel_dim, e->proj_out.Npad, a->pred, c.st));
+  HIPCK(copy_pred(c.b.p, c.S, c.L, e->a.backbone == F5H_DIT ? 0 : 1, e->a.mel_dim, e->proj_out.Npad, a->pred,
+                  c.chain ? e->chain_fault : nullptr, c.st));
+  if (c.chain) RC(chain_fault_note(e, c.st));
   return 0;
 }
 
@@ -1582,13 +1769,33 @@ int f5h_set_chain(f5h_engine* e, int32_t enable) {
   return 0;
 }
 
-int f5h_chain_stats(int64_t* launches, int32_t* fault) {
-  if (launches) *launches = f5h::chain_launches();
+int f5h_chain_stats(f5h_engine* e, int64_t* launches, int32_t* fault, int64_t* refused) {
+  if (!e) return fail(F5H_EINVAL, "null engine");
+  if (launches) *launches = e->n_chain.load(std::memory_order_relaxed);
+  if (refused) *refused = g_gate_refused.load(std::memory_order_relaxed);
   if (fault) {
-    const int f = f5h::chain_fault_take();
-    if (f < 0) return fail(F5H_EHIP, "chain fault word unreadable");
-    *fault = f;
+    *fault = 0;
+    if (e->chain_fault) {  // the caller has synchronised with the engine's calls (the device word is final)
+      unsigned v = 0;
+      HIPCK(hipSetDevice(e->dev));
+      HIPCK(hipMemcpyAsync(&v, e->chain_fault, sizeof(v), hipMemcpyDeviceToHost, e->mstream));
+      HIPCK(hipStreamSynchronize(e->mstream));
+      *fault = v ? 1 : 0;
+    }
   }
+  return 0;
+}
+
+int f5h_last_call_host_ms(f5h_engine* e, double* ms, int32_t n) {
+  if (!e || !ms || n <= 0) return fail(F5H_EINVAL, "null engine / buffer");
+  std::lock_guard<std::mutex> g(e->hm);
+  for (int i = 0; i < n; ++i) ms[i] = i < kHostPhases ? e->last_host[i] : 0.0;
+  return 0;
+}
+
+int f5h_chain_debug_spin_limit(int64_t limit) {
+  chain_set_spin_limit(limit);
+  g_kernel_epoch.fetch_add(1);  // captured graphs hold the old kernel arguments
   return 0;
 }
 

@@ -992,7 +992,7 @@ F5H_DEV void gemm_body(const GemmArgs& g, const int b, const int nwg, uint4* lds
   // the strip loop covers an older store (one strip of global round trips instead of one per
   // chunk; measured 9.5 us of a 30.6 us QKV launch before).
   constexpr bool FAST_EPI = FAST && NT % 2 == 0;
-  static_assert(FAST_EPI || !PUB, "the chain publishes from the direct epilogue");
+  static_assert(FAST_EPI || !PUB, "the chain publishes after the fast (LDS-strip) epilogue");
   if constexpr (FAST_EPI) {
     epilogue_fast<TC, EPI, MT, NT, WN, C::EPAD, PREF, PUB ? kAuxWT : 0>(g, acc, Cs, m0 + wm * WM, n0 + wn * WN, lane,
                                                                          pre);

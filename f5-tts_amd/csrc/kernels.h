@@ -86,7 +86,7 @@ __host__ __device__ inline bool tile_live_rows(const int32_t* live_len, int live
 
 // compute: ComputeMode (fp32 / bf16 / fp16 operands). A and W both in the operand dtype.
 hipError_t gemm(int compute, int epi, const GemmArgs& a, hipStream_t st);
-// pin the 16-bit GEMM tile configuration (0, 1, 5, 11; -1 = automatic choice); tuning and test hook
+// pin the 16-bit GEMM tile configuration (0, 1, 5, 11, 12, 13; -1 = automatic choice); tuning and test hook
 void gemm_force_config(int cfg);
 
 // attention: Q,K,V [S,H,L,64] operand dtype; O [S,L,H*64] operand dtype.
@@ -187,8 +187,9 @@ hipError_t stamp_end(unsigned long long* slots, const int* tick, hipStream_t st)
 hipError_t step_advance(int* kstep, int* tick, hipStream_t st);
 hipError_t final_where(const float* cond, const uint8_t* cond_mask, float* y, int B, int N, int mel,
                        hipStream_t st);
+// fault: the phase-chain give-up word (or null); when set, out is filled with NaN (the results are wrong)
 hipError_t final_where_out(const float* cond, const uint8_t* cond_mask, const float* y, float* out, int B, int N,
-                           int mel, hipStream_t st);
+                           int mel, const unsigned* fault, hipStream_t st);
 // *slot = p (stream-ordered)
 hipError_t ptr_upload(float* p, float** slot, hipStream_t st);
 // rowkeep[s*L + pos] = (pos - off < dur[s % B]) || pos < off ; for S sequences
@@ -197,8 +198,9 @@ hipError_t build_rowkeep(const int32_t* dur, int B, int S, int L, int off, uint8
 hipError_t build_kvlen(const int32_t* dur, int B, int S, int off, int32_t* kv, hipStream_t st);
 // h[s, 0, :] = temb (UNetT time token)
 hipError_t write_time_token(int compute, int h16, const float* temb, int S, int L, int d, void* h, hipStream_t st);
-// extract rows [s, 1..L-1] of pred -> dst [S, L-1, mel]
-hipError_t copy_pred(const float* p, int S, int L, int row_off, int mel, int64_t p_ld, float* dst, hipStream_t st);
+// extract rows [s, 1..L-1] of pred -> dst [S, L-1, mel]; NaN when *fault (as final_where_out)
+hipError_t copy_pred(const float* p, int S, int L, int row_off, int mel, int64_t p_ld, float* dst,
+                     const unsigned* fault, hipStream_t st);
 // Vocos decoder glue (vocos.hip)
 hipError_t vocos_im2col(int compute, const float* mel, int B, int T, int C, int Kp, void* out, hipStream_t st);
 hipError_t vocos_spec(float* x, int64_t rows, int bins, int ld, hipStream_t st);
@@ -229,7 +231,8 @@ struct ChainDep {
   const unsigned* wait;  // the producer phase's row-group counters (null: no in-launch producer)
   int wait_mult, wait_unit;  // a complete group holds wait_mult * ceil(rows of the group / wait_unit) arrivals
   unsigned* pub;         // this phase's row-group counters (null: last phase)
-  unsigned* err;         // set to 1 when a wait gives up (bounded spin); the results are then garbage
+  unsigned* err;         // the engine's fault word: set to 1 when a wait gives up (bounded spin); results then wrong
+  unsigned spin_limit;   // polls before a wait gives up
   unsigned long long* tl;  // (set per workgroup in the kernel) its timeline row when the launch is probed, or null
 };
 struct LnArgs {
@@ -243,19 +246,21 @@ struct ChainArgs {
   LnArgs ln1, ln2;
   unsigned* cnt;   // [5][groups] arrival counters, zero before the launch
   int groups;      // ceil(M / kChainRows) (stride of cnt)
+  unsigned* fault; // the engine's give-up word (device): a wait that gives up sets it to 1 (f5h_sample then
+                   // returns NaN in `out`, and the engine's next call fails with F5H_EHIP)
   DevProbe probe;  // launch timing (f5h_probe_enable "chain"); timeline row per workgroup: entry, rows acquired,
                    // results stored, exit
 };
-// bytes of cnt a chain launch over M rows uses (the caller zeroes them before every launch)
+// bytes of cnt a chain launch over M rows uses (the caller zeroes them before the first layer's launch of a step:
+// every layer's launch has its own [5][groups] block)
 inline size_t chain_counter_bytes(int M) {
   return (size_t)5 * ((M + kChainRows - 1) / kChainRows) * sizeof(unsigned);
 }
 // Launch the chain (16-bit operands, dim 1024, whole-column tiles); hipErrorInvalidValue when the shapes do not
 // fit it (the caller then issues the separate launches).
 hipError_t chain_launch(int compute, const ChainArgs& a, hipStream_t st);
-// the give-up word of the chain's bounded waits: returns it and clears it (host call, synchronous)
-int chain_fault_take();
-// chain launches enqueued by this process
-int64_t chain_launches();
+// polls before a chain wait gives up: kChainSpinLimit by default; test hook (f5h_chain_debug_spin_limit) to force
+// give-ups, -1 restores the default. Read at launch (graphs captured earlier keep their value)
+void chain_set_spin_limit(long long limit);
 
 }  // namespace f5h

@@ -1,7 +1,9 @@
 // Reaper thread for the deferred release of device resources (reaper.h).
 #include "reaper.h"
 
+#include <cerrno>
 #include <condition_variable>
+#include <cstdio>
 #include <cstdlib>
 #include <deque>
 #include <system_error>
@@ -73,7 +75,17 @@ hipMemPool_t pool_of(int dev) {
   // f5h_release_pending(2) (Python: f5_tts_amd.release_memory()) returns it; F5H_POOL_KEEP_MB=<n> caps what
   // the pool keeps past a synchronisation point instead (memory).
   uint64_t keep = ~0ull;
-  if (const char* kv = getenv("F5H_POOL_KEEP_MB")) keep = (uint64_t)strtoull(kv, nullptr, 10) << 20;
+  if (const char* kv = getenv("F5H_POOL_KEEP_MB")) {
+    // applied only when the whole value is a number of MB: anything else ("", "off", "inf", "12x") would parse as
+    // 0 and trim the pool at every synchronisation point, the opposite of the default
+    char* end = nullptr;
+    errno = 0;
+    const unsigned long long mb = strtoull(kv, &end, 10);
+    if (*kv && end && *end == '\0' && errno == 0 && mb < (1ull << 44))
+      keep = (uint64_t)mb << 20;
+    else
+      std::fprintf(stderr, "[f5h] F5H_POOL_KEEP_MB=\"%s\" is not a number of MB: ignored (the pool keeps all)\n", kv);
+  }
   (void)hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &keep);
   g_pools.emplace_back(dev, pool);
   return pool;

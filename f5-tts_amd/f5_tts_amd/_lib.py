@@ -38,9 +38,11 @@ EXPORTS = (
     "f5h_set_graph_mode",
     "f5h_set_cfg_streams",
     "f5h_graph_stats",
+    "f5h_last_call_host_ms",
     "f5h_set_pad_skip",
     "f5h_set_chain",
     "f5h_chain_stats",
+    "f5h_chain_debug_spin_limit",
     "f5h_op_linear",
     "f5h_op_attention",
     "f5h_gemm_force_config",
@@ -151,6 +153,9 @@ def lib():
     L.f5h_set_cfg_streams.restype = ctypes.c_int
     L.f5h_graph_stats.argtypes = [vp, ctypes.POINTER(i64), ctypes.POINTER(i64), ctypes.POINTER(i32)]
     L.f5h_graph_stats.restype = ctypes.c_int
+    if hasattr(L, "f5h_last_call_host_ms"):
+        L.f5h_last_call_host_ms.argtypes = [vp, ctypes.POINTER(ctypes.c_double), i32]
+        L.f5h_last_call_host_ms.restype = ctypes.c_int
     L.f5h_set_pad_skip.argtypes = [vp, i32]
     L.f5h_set_pad_skip.restype = ctypes.c_int
     L.f5h_op_linear.argtypes = [vp, i32, i32, i32, i32, vp, vp, vp, vp, vp, sz]
@@ -166,8 +171,11 @@ def lib():
     if hasattr(L, "f5h_set_chain"):
         L.f5h_set_chain.argtypes = [vp, i32]
         L.f5h_set_chain.restype = ctypes.c_int
-        L.f5h_chain_stats.argtypes = [ctypes.POINTER(i64), ctypes.POINTER(i32)]
+        L.f5h_chain_stats.argtypes = [vp, ctypes.POINTER(i64), ctypes.POINTER(i32), ctypes.POINTER(i64)]
         L.f5h_chain_stats.restype = ctypes.c_int
+    if hasattr(L, "f5h_chain_debug_spin_limit"):
+        L.f5h_chain_debug_spin_limit.argtypes = [i64]
+        L.f5h_chain_debug_spin_limit.restype = ctypes.c_int
     if hasattr(L, "f5h_debug_tile_live"):
         L.f5h_debug_tile_live.argtypes = [vp, i32, i32, i32, i32]
         L.f5h_debug_tile_live.restype = ctypes.c_int

@@ -131,6 +131,23 @@ class Engine:
         path without row masks; f5h_set_chain; default on). Results are bitwise identical either way."""
         _lib.check(_lib.lib().f5h_set_chain(self._h, int(bool(on))), "set_chain")
 
+    def chain_stats(self):
+        """(phase-chain launches this engine enqueued, 1 if one of its chain waits gave up and the engine has not
+        reported it yet, chained calls of this process that the per-device concurrency rule sent to the separate
+        launches). Synchronous; call after the engine's work has completed (f5h_chain_stats)."""
+        n, f, r = ctypes.c_int64(), ctypes.c_int32(), ctypes.c_int64()
+        _lib.check(_lib.lib().f5h_chain_stats(self._h, ctypes.byref(n), ctypes.byref(f), ctypes.byref(r)),
+                   "chain_stats")
+        return int(n.value), int(f.value), int(r.value)
+
+    HOST_PHASES = ("total", "prologue", "cache_lock", "reap", "capture", "instantiate", "launch", "final")
+
+    def last_call_host_ms(self):
+        """Host milliseconds of this engine's newest sample call by phase (f5h_last_call_host_ms)."""
+        buf = (ctypes.c_double * 8)()
+        _lib.check(_lib.lib().f5h_last_call_host_ms(self._h, buf, 8), "last_call_host_ms")
+        return {k: round(buf[i], 4) for i, k in enumerate(self.HOST_PHASES)}
+
     def graph_stats(self):
         cap, rep, n = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int32()
         _lib.check(_lib.lib().f5h_graph_stats(self._h, ctypes.byref(cap), ctypes.byref(rep), ctypes.byref(n)),
@@ -285,13 +302,11 @@ def attn_force_safe(on: bool):
 
 
 def gemm_force_config(cfg: int = -1):
-    """Pin the 16-bit GEMM tile configuration (0, 1, 5, 11) for this process; -1 = automatic."""
+    """Pin the 16-bit GEMM tile configuration (0, 1, 5, 11, 12, 13) for this process; -1 = automatic."""
     _lib.check(_lib.lib().f5h_gemm_force_config(int(cfg)), "gemm_force_config")
 
 
-def chain_stats():
-    """Test hook: (phase-chain launches enqueued by this process, 1 if one gave up waiting for a producer since
-    the last call, else 0; cleared)."""
-    n, f = ctypes.c_int64(), ctypes.c_int32()
-    _lib.check(_lib.lib().f5h_chain_stats(ctypes.byref(n), ctypes.byref(f)), "chain_stats")
-    return int(n.value), int(f.value)
+def chain_debug_spin_limit(limit: int = -1):
+    """Test hook: polls before a phase-chain wait gives up (0: at the first poll that finds its rows not yet
+    produced); -1 restores the default (~0.3 s). Applies to launches and graph captures made afterwards."""
+    _lib.check(_lib.lib().f5h_chain_debug_spin_limit(int(limit)), "chain_debug_spin_limit")

@@ -210,6 +210,11 @@ int f5h_set_graph_mode(f5h_engine* eng, int32_t mode);
  * creation). Results are bitwise identical. */
 int f5h_set_cfg_streams(f5h_engine* eng, int32_t n);
 int f5h_graph_stats(f5h_engine* eng, int64_t* captures, int64_t* replays, int32_t* cached);
+/* Host milliseconds the engine's newest f5h_sample call spent, by phase (a call that blocks its host thread
+ * shows where): ms[0] whole call, [1] prologue (enqueue, or graph stage + launch), [2] waiting for the graph
+ * cache lock, [3] destroying evicted graphs, [4] capturing, [5] instantiating, [6] launching the step graphs /
+ * steps, [7] final kernel + fault-word copy. Writes min(n, 8) values, zeros past 8. */
+int f5h_last_call_host_ms(f5h_engine* eng, double* ms, int32_t n);
 /* Batch path (use_batch_mask): pad query rows' attention output is zeroed after to_out
  * (modules.py:551-553), so attention query blocks past a sequence's length exit at entry and out-proj row
  * tiles of padding only skip their work (the rows keep their residual, as masked rows of a computed tile
@@ -220,10 +225,20 @@ int f5h_set_pad_skip(f5h_engine* eng, int32_t enable);
  * arrival counters (chain.hip, DESIGN.md §3 'Phase chain'), instead of six launches. 1 (default) or 0 (env
  * F5H_CHAIN=0 at creation: 0). Bitwise identical results. */
 int f5h_set_chain(f5h_engine* eng, int32_t enable);
-/* Test hook: *launches = phase-chain launches this process has enqueued (eager launches and graph captures);
- * *fault = 1 if one of them gave up waiting for a producer (a bounded wait that should never expire; its
- * results are then wrong), else 0; the flag is cleared. Synchronous. Either pointer may be NULL. */
-int f5h_chain_stats(int64_t* launches, int32_t* fault);
+/* Failure of the chain (never expected): a chain wait that gives up (a bounded spin of ~0.3 s) sets the
+ * ENGINE's fault word; that call's `out` (f5h_sample) / `pred` (f5h_forward) is then all NaN, and the engine's
+ * next f5h_sample / f5h_forward fails with F5H_EHIP (message in f5h_last_error), clears the word and turns the
+ * chain off for the engine. Concurrency: a call that would chain while a chained call from another stream of
+ * the same device is still enqueued or running takes the separate launches (two chain launches in flight starve
+ * each other, DESIGN.md §3 'Phase chain'); results are bitwise the same either way.
+ * Test hook: *launches = chain launches this engine has enqueued (eager launches and graph captures);
+ * *fault = the engine's fault word (1: a wait gave up since it was last cleared; NOT cleared here: the next call
+ * reports it); *refused = chained calls of this process sent to the separate launches by the concurrency rule.
+ * Synchronous; call after the engine's work has completed. Any pointer may be NULL. */
+int f5h_chain_stats(f5h_engine* eng, int64_t* launches, int32_t* fault, int64_t* refused);
+/* Test hook: polls before a chain wait gives up (limit >= 0; 0 = at the first poll that finds its rows not yet
+ * produced), -1 restores the default (~0.3 s). Applies to launches and graph captures made afterwards. */
+int f5h_chain_debug_spin_limit(int64_t limit);
 
 /* Op-level entry points (parity tests / microbenchmarks). Device pointers, row-major. */
 /* C[M,N] = A[M,K] . W[N,K]^T + bias  (fp32 in/out; compute = F5H_FP32 or F5H_BF16 operands) */
