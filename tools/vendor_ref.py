@@ -4,8 +4,12 @@
 get the per-kernel averages; also prints / writes event-timed averages per op (20 back-to-back launches).
 
   python tools/vendor_ref.py [out.json]
+
+VENDOR_GEMM_ONLY=1 skips SDPA and VENDOR_REPS=n fixes the timed launches per op (3 warm + n each, in SH order:
+tools/vendor_pmc.py maps counter-pass dispatches to ops by that order).
 """
 import json
+import os
 import sys
 
 import torch
@@ -40,13 +44,14 @@ g = torch.Generator(device=dev).manual_seed(0)
 for name, (M, N, K) in SH.items():
     A = torch.randn(M, K, device=dev, dtype=torch.bfloat16, generator=g)
     W = torch.randn(N, K, device=dev, dtype=torch.bfloat16, generator=g)
-    us = timed(lambda: A @ W.t(), 20 if M < 10000 else 5)
+    reps = int(os.environ.get("VENDOR_REPS", "0")) or (20 if M < 10000 else 5)
+    us = timed(lambda: A @ W.t(), reps)
     tf = 2 * M * N * K / us / 1e6
     res["ops"][name] = {"kind": "hipBLASLt torch.mm bf16", "M": M, "N": N, "K": K, "us": us, "tflops": tf,
                         "frac": tf / 2500.0}
     print(f"{name}: {us:.1f} us  {tf:.0f} TF/s", flush=True)
     del A, W
-for cfg, S in (("c2", 2), ("c4", 64)):
+for cfg, S in (() if os.environ.get("VENDOR_GEMM_ONLY") == "1" else (("c2", 2), ("c4", 64))):
     q, k, v = (torch.randn(S, 16, N_FR, 64, device=dev, dtype=torch.bfloat16, generator=g) for _ in range(3))
     us = timed(lambda: F.scaled_dot_product_attention(q, k, v), 10 if S < 10 else 3)
     tf = 4 * S * 16 * N_FR * N_FR * 64 / us / 1e6
