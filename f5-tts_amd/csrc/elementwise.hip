@@ -120,6 +120,19 @@ hipError_t step_advance(int* kstep, int* tick, hipStream_t st) {
   return hipGetLastError();
 }
 
+// p[0..n) = 0 by vector stores (the phase chain's arrival counters, zeroed ahead of every step)
+__global__ void zero_words_kernel(uint4* p, int64_t n4) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (int64_t)gridDim.x * blockDim.x)
+    p[i] = uint4{0u, 0u, 0u, 0u};
+}
+hipError_t zero_words(unsigned* p, int64_t n, hipStream_t st) {
+  if (n % 4 || ((uintptr_t)p & 15)) return hipErrorInvalidValue;
+  const int64_t n4 = n / 4;
+  hipLaunchKernelGGL(zero_words_kernel, dim3((unsigned)std::min<int64_t>(64, nblk(n4, 256))), dim3(256), 0, st,
+                     reinterpret_cast<uint4*>(p), n4);
+  return hipGetLastError();
+}
+
 template <typename TO>
 __global__ void silu_kernel(const float* x, TO* y, int64_t n) {
   int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;

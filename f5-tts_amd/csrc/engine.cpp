@@ -808,7 +808,16 @@ static int backbone_part(Ctx& c, int s0, int ns, hipStream_t st) {
   const bool chain_on = c.chain && dit && r16 && do_ln && !keep && d == 1024 && b.chain && s0 == 0 && ns == c.S &&
                         (e->probe_class < 0 || e->probe_class == KC_ATTN || e->probe_class == KC_CONV ||
                          e->probe_class == KC_CHAIN);
-  if (chain_on) KCK(hipMemsetAsync(b.chain, 0, (size_t)a.depth * 5 * b.chain_g4 * sizeof(unsigned), st));
+  static const bool zero_memset = [] {  // F5H_CHAIN_ZERO=memset: the counters zeroed by a memset node (A/B)
+    const char* v = getenv("F5H_CHAIN_ZERO");
+    return v && !strcmp(v, "memset");
+  }();
+  if (chain_on) {
+    if (zero_memset)
+      KCK(hipMemsetAsync(b.chain, 0, (size_t)a.depth * 5 * b.chain_g4 * sizeof(unsigned), st));
+    else
+      KCK(zero_words(b.chain, (int64_t)a.depth * 5 * b.chain_g4, st));
+  }
   bool qkv_done = false;    // this layer's LayerNorm + QKV came with the previous layer's chain
   bool final_done = false;  // the final LayerNorm came with the last layer's chain
   for (int l = 0; l < a.depth; ++l) {

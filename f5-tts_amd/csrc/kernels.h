@@ -185,6 +185,8 @@ hipError_t stamp_begin(unsigned long long* slots, const int* tick, hipStream_t s
 hipError_t stamp_end(unsigned long long* slots, const int* tick, hipStream_t st);
 // *kstep += 1 and *tick += 1 (probe step tick)
 hipError_t step_advance(int* kstep, int* tick, hipStream_t st);
+// p[0..n) = 0 (n a multiple of 4, p 16-B aligned): a kernel, not a memset node
+hipError_t zero_words(unsigned* p, int64_t n, hipStream_t st);
 hipError_t final_where(const float* cond, const uint8_t* cond_mask, float* y, int B, int N, int mel,
                        hipStream_t st);
 // fault: the phase-chain give-up word (or null); when set, out is filled with NaN (the results are wrong)

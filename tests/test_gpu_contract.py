@@ -624,25 +624,59 @@ def test_phase_chain_bitwise_equal(compute):
                 eng.set_chain(mode != "plain")
                 eng.set_graph_mode(mode != "chain_eager")
                 eng.set_cfg_streams(2 if mode == "chain_two" else 1)
-                n0, _, _ = eng.chain_stats()
-                out, traj = m.sample(**kw)
-                torch.cuda.synchronize()
-                n1, fault, _ = eng.chain_stats()
-                assert fault == 0, (total, mode)
-                if mode == "chain_eager":
-                    assert n1 - n0 == 4 * arch["depth"], (total, mode, n1 - n0)  # every layer of every step
-                elif mode == "chain":
-                    assert n1 - n0 in (0, arch["depth"]), (total, mode, n1 - n0)  # a capture (or a cached graph)
-                else:  # plain, and the two-stream parts (chain off)
-                    assert n1 == n0, (total, mode, n1 - n0)
-                outs[mode] = (out.clone(), traj.clone())
-            for mode in ("chain", "chain_eager", "chain_two"):
-                assert torch.equal(outs[mode][0], outs["plain"][0]), (total, mode)
-                assert torch.equal(outs[mode][1], outs["plain"][1]), (total, mode)
+                for rep in range(3):  # the first call of a graph key captures; the later ones only replay
+                    n0, _, _ = eng.chain_stats()
+                    out, traj = m.sample(**kw)
+                    torch.cuda.synchronize()
+                    n1, fault, _ = eng.chain_stats()
+                    assert fault == 0, (total, mode, rep)
+                    if mode == "chain_eager":
+                        assert n1 - n0 == 4 * arch["depth"], (total, mode, n1 - n0)  # every layer of every step
+                    elif mode == "chain":
+                        assert n1 - n0 in (0, arch["depth"]), (total, mode, n1 - n0)  # a capture (or a cached graph)
+                    else:  # plain, and the two-stream parts (chain off)
+                        assert n1 == n0, (total, mode, n1 - n0)
+                    outs[(mode, rep)] = (out.clone(), traj.clone())
+            for mode in ("plain", "chain", "chain_eager", "chain_two"):
+                for rep in range(3):
+                    assert torch.equal(outs[(mode, rep)][0], outs[("plain", 0)][0]), (total, mode, rep)
+                    assert torch.equal(outs[(mode, rep)][1], outs[("plain", 0)][1]), (total, mode, rep)
     finally:
         eng.set_chain(True)
         eng.set_graph_mode(True)
         eng.set_cfg_streams(0)
+
+
+@pytest.mark.parametrize("compute", ["bf16", "fp16"])
+def test_phase_chain_c2_graph_replays_bitwise_equal(compute):
+    """C2 at full size (F5 v1 Base, 938 + 938 frames, NFE 16): repeated calls replaying the captured step graph with
+    the phase chain give bitwise the unchained result, call after call. Round 6 found that the chain's arrival
+    counters, zeroed by a captured hipMemsetAsync node, were not re-zeroed on the replays of later calls (ROCm 7.2):
+    every call after the capturing one skipped its waits and returned wrong audio (~9 % rel-L2) with no error. The
+    counters are now zeroed by a kernel of the step graph (engine.cpp backbone_part)."""
+    _need_gpu()
+    arch = configs.get_arch("F5TTS_v1_Base")
+    m = _model(arch, compute)
+    eng = m.transformer.get_engine(compute, m.device)
+    inp = synthetic.make_case(**gc.C2)
+    dur = torch.maximum(torch.maximum((inp["text"] != -1).sum(-1), inp["lens"]) + 1, inp["duration"])
+    y0 = synthetic.reference_noise(dur, gc.SEED)
+    kw = dict(cond=inp["cond"].to(DEV), text=inp["text"].to(DEV), duration=inp["duration"], lens=inp["lens"],
+              steps=16, cfg_strength=2.0, sway_sampling_coef=-1.0, y0=y0.to(DEV), keep_trajectory=False)
+    try:
+        eng.set_chain(False)
+        plain = m.sample(**kw)[0].clone()
+        eng.set_chain(True)
+        n0 = eng.chain_stats()[0]
+        outs = [m.sample(**kw)[0].clone() for _ in range(4)]
+        torch.cuda.synchronize()
+        n1, fault, _ = eng.chain_stats()
+    finally:
+        eng.set_chain(True)
+    assert n1 - n0 == arch["depth"], "one capture of the chained step graph, replayed by every call"
+    assert fault == 0
+    for i, o in enumerate(outs):
+        assert torch.equal(o, plain), (i, gc.rel_err(o.float().cpu().numpy(), plain.float().cpu().numpy()))
 
 
 def _chain_case(arch, total, seed):

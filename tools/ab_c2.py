@@ -4,7 +4,8 @@ arm's output is bitwise identical to the first arm's.
 
     python tools/ab_c2.py [--config c2] [--rounds 5] [--calls 5] [--arms streams1,streams2]
 Arms: streams1 / streams2 (f5h_set_cfg_streams), gemmN (f5h_gemm_force_config N, -1 = auto),
-eager (step graph off).
+eager (step graph off), chain0 / chain1 (f5h_set_chain). Outputs are compared for the warm call (a graph capture)
+AND the last timed call of every arm (graph replays only: round 6 found a bug that only replays showed).
 """
 import argparse
 import os
@@ -46,8 +47,10 @@ def main():
         eng.set_graph_mode(arm != "eager")
         eng.set_cfg_streams(1 if arm == "streams1" else (2 if arm == "streams2" else 0))
         gemm_force_config(int(arm[4:]) if arm.startswith("gemm") else -1)
+        if arm.startswith("chain"):
+            eng.set_chain(arm == "chain1")
 
-    outs, times = {}, {arm: [] for arm in arms}
+    outs, lasts, times = {}, {}, {arm: [] for arm in arms}
     for arm in arms:  # warm every arm (graph capture) before timing
         setup(arm)
         outs[arm] = model.sample(**kw)[0].clone()
@@ -59,15 +62,16 @@ def main():
             torch.cuda.synchronize()
             t0 = time.perf_counter()
             for _ in range(a.calls):
-                model.sample(**kw)
+                last = model.sample(**kw)[0]
             torch.cuda.synchronize()
+            lasts[arm] = last.clone()
             times[arm].append((time.perf_counter() - t0) / a.calls * 1e3)
     setup(arms[0])
     for arm in arms:
         t = sorted(times[arm])
-        same = torch.equal(outs[arm], outs[arms[0]])
-        print(f"{arm:10s} median {t[len(t) // 2]:8.3f} ms  min {t[0]:8.3f} ms  bitwise-equal-to-{arms[0]} {same}",
-              flush=True)
+        same = torch.equal(outs[arm], outs[arms[0]]) and torch.equal(lasts[arm], outs[arms[0]])
+        print(f"{arm:10s} median {t[len(t) // 2]:8.3f} ms  min {t[0]:8.3f} ms  bitwise-equal-to-{arms[0]} {same} "
+              f"(warm and last timed call)", flush=True)
 
 
 if __name__ == "__main__":
