@@ -120,9 +120,11 @@ struct f5h_engine {
   // skip the dead pad-row work of the batch path (attention query blocks and out-proj row tiles of padding
   // only): f5h_set_pad_skip, env F5H_NO_PAD_SKIP=1 at creation turns it off. Bitwise identical results.
   int pad_skip = 1;
-  // In-launch phase chain of the DiT block-step's row-local seams (chain.hip): f5h_set_chain, env F5H_CHAIN=0 at
-  // creation turns it off. Bitwise identical results.
-  int chain = 1;
+  // In-launch phase chain of the DiT block-step's row-local seams (chain.hip): f5h_set_chain, env F5H_CHAIN=1 at
+  // creation turns it on. Bitwise identical results. OFF by default since round 6: with its counters correctly
+  // re-zeroed on every graph replay it measured C2 58.4 vs 51.1 ms unchained (profiles/r06_ab_chain_c2.txt); the
+  // round-5 gain came from a captured memset node that later replays did not apply (waits skipped, wrong results).
+  int chain = 0;
   // The chain's give-up word (chain.h): device memory of the engine, set by a chain wait that expired. The call's final
   // kernel then writes NaN results; a copy of it lands in a pinned host word (fault_host) at the end of every chained
   // call, and the engine's next call reads that word, fails with F5H_EHIP and switches the chain off.
@@ -1141,7 +1143,7 @@ int f5h_engine_create_views(const f5h_arch* arch, const f5h_tensor_view* weights
   if (const char* gv = getenv("F5H_GRAPH")) e->graph_mode = atoi(gv) ? 1 : 0;
   if (const char* sv = getenv("F5H_SPLIT_CFG")) e->split_cfg = std::min(2, std::max(0, atoi(sv)));
   if (const char* pv = getenv("F5H_NO_PAD_SKIP")) e->pad_skip = (*pv == '1') ? 0 : 1;
-  if (const char* cv = getenv("F5H_CHAIN")) e->chain = (*cv == '0') ? 0 : 1;
+  if (const char* cv = getenv("F5H_CHAIN")) e->chain = (*cv == '1') ? 1 : 0;
   // device views are read on the engine's non-blocking stream: order it behind the null stream (so behind
   // every blocking stream's queued work, the ordering the packing had when it ran on the null stream); work
   // on other non-blocking streams must be complete (f5h.h)

@@ -222,8 +222,9 @@ int f5h_last_call_host_ms(f5h_engine* eng, double* ms, int32_t n);
 int f5h_set_pad_skip(f5h_engine* eng, int32_t enable);
 /* 16-bit DiT path without row masks: run each layer's out-proj, LayerNorm, FFN1, FFN2 and the next layer's
  * LayerNorm + QKV (modules.py:743-757) as ONE launch whose phases hand 64-row groups to each other through
- * arrival counters (chain.hip, DESIGN.md §3 'Phase chain'), instead of six launches. 1 (default) or 0 (env
- * F5H_CHAIN=0 at creation: 0). Bitwise identical results. */
+ * arrival counters (chain.hip, DESIGN.md §3 'Phase chain'), instead of six launches. 0 (default) or 1 (env
+ * F5H_CHAIN=1 at creation: 1). Bitwise identical results; slower than the separate launches at C2 (58.4 vs
+ * 51.1 ms), hence off. */
 int f5h_set_chain(f5h_engine* eng, int32_t enable);
 /* Failure of the chain (never expected): a chain wait that gives up (a bounded spin of ~0.3 s) sets the
  * ENGINE's fault word; that call's `out` (f5h_sample) / `pred` (f5h_forward) is then all NaN, and the engine's

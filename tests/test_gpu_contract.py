@@ -642,7 +642,7 @@ def test_phase_chain_bitwise_equal(compute):
                     assert torch.equal(outs[(mode, rep)][0], outs[("plain", 0)][0]), (total, mode, rep)
                     assert torch.equal(outs[(mode, rep)][1], outs[("plain", 0)][1]), (total, mode, rep)
     finally:
-        eng.set_chain(True)
+        eng.set_chain(False)
         eng.set_graph_mode(True)
         eng.set_cfg_streams(0)
 
@@ -672,7 +672,7 @@ def test_phase_chain_c2_graph_replays_bitwise_equal(compute):
         torch.cuda.synchronize()
         n1, fault, _ = eng.chain_stats()
     finally:
-        eng.set_chain(True)
+        eng.set_chain(False)
     assert n1 - n0 == arch["depth"], "one capture of the chained step graph, replayed by every call"
     assert fault == 0
     for i, o in enumerate(outs):
@@ -723,7 +723,7 @@ def test_phase_chain_give_up_fails_loudly():
         assert torch.equal(again, plain)
     finally:
         chain_debug_spin_limit(-1)
-        eng.set_chain(True)
+        eng.set_chain(False)
     fixed, _ = m.sample(**kw)
     torch.cuda.synchronize()
     assert torch.equal(fixed, plain) and eng.chain_stats()[1] == 0
@@ -742,6 +742,7 @@ def test_phase_chain_concurrent_streams():
     arch = configs.get_arch("F5TTS_v1_Base", depth=3)
     m = _model(arch, "bf16")
     eng = m.transformer.get_engine("bf16", m.device)
+    eng.set_chain(True)  # (off by default)
     cases = [[_chain_case(arch, 1876, 10 + 2 * t + i) for i in range(3)] for t in range(2)]
     streams = [torch.cuda.Stream(), torch.cuda.Stream()]
 

@@ -79,7 +79,6 @@ def _envelope(case, lo_fixture, compute):
     tag, spec, nfe, sway, cfg = gc.SAMPLE_CASES[case]
     m = _model(gc.arch_of(tag), compute)
     eng = m.transformer.get_engine(compute, m.device)
-    n0 = eng.chain_stats()[0]
     inp = synthetic.make_case(**spec)
     dur = torch.maximum(torch.maximum((inp["text"] != -1).sum(-1), inp["lens"]) + 1, inp["duration"])
     y0 = synthetic.reference_noise(dur, gc.SEED)
@@ -87,11 +86,8 @@ def _envelope(case, lo_fixture, compute):
                       lens=inp["lens"].to(DEV), steps=nfe, cfg_strength=cfg, sway_sampling_coef=sway,
                       y0=y0.to(DEV), keep_trajectory=False)
     out = out.float().cpu().numpy()
-    # the phase chain (on for the 16-bit single-utterance DiT calls: C2, C1) ran and none of its waits gave up
-    n1, fault, _ = eng.chain_stats()
-    assert fault == 0, case
-    if case == "c2_sample_fp32":  # C2 in bf16/fp16: the chain's shape (DiT, dim 1024, one utterance)
-        assert n1 > n0, (case, compute, "the chain did not run")
+    # no phase-chain wait gave up (the chain is off by default; F5H_CHAIN=1 runs these cases through it)
+    assert eng.chain_stats()[1] == 0, case
     assert out.shape == f32["out"].shape
     assert np.isfinite(out).all()
     ref32 = _gen_frames(f32["out"], inp["lens"], dur)
