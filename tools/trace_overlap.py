@@ -29,16 +29,13 @@ def main(trace, line_path, out):
     line = json.loads(open(line_path).read().strip().splitlines()[-1])
     steps = line["steps"]
     # the timed calls are the last `steps` calls: each call has nfe x depth chain launches (C2: 16 x 22 = 352)
-    chains = [i for i, d in enumerate(disp) if "chain_kernel" in d[2]]
-    per_call = 352
-    if len(chains) < steps * per_call:
-        raise SystemExit(f"{len(chains)} chain dispatches, fewer than {steps} calls x {per_call}")
-    first = chains[-steps * per_call]
-    # the window: from the first timed call's first dispatch (its prologue precedes its first chain launch by the
-    # conv/QKV/attention launches of layer 0: start the window at the previous euler launch's end)
-    j = first
-    while j > 0 and "cfg_euler" not in disp[j - 1][2]:
-        j -= 1
+    # each call ends its NFE steps with one cfg_euler launch per step (C2: 16); the timed calls are the last `steps`
+    # calls: the window starts right after the euler launch that ended the call before them
+    eul = [i for i, d in enumerate(disp) if "cfg_euler" in d[2]]
+    nfe = 16
+    if len(eul) < (steps + 1) * nfe:
+        raise SystemExit(f"{len(eul)} euler dispatches, fewer than {steps + 1} calls x {nfe}")
+    j = eul[-steps * nfe - 1] + 1
     win = disp[j:]
     t0, t1 = win[0][0], max(e for _, e, _ in win)
     by = {}
@@ -61,7 +58,7 @@ def main(trace, line_path, out):
     busy += cur_e - cur_s
     ssum = sum(e - s for s, e, _ in win)
     res = {
-        "note": "rocprofv3 --kernel-trace of bench.py (C2, chain on, --probe none) over the timed calls' window",
+        "note": "rocprofv3 --kernel-trace of bench.py (C2, --probe none) over the timed calls' window (from the end of the last untimed call's final Euler launch)",
         "calls": steps, "bench_ms_per_step_under_profiler": line["ms_per_step"],
         "window_ms_per_call": round((t1 - t0) / 1e6 / steps, 3),
         "sum_of_durations_ms_per_call": round(ssum / 1e6 / steps, 3),
