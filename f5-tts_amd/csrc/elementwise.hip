@@ -120,6 +120,74 @@ hipError_t step_advance(int* kstep, int* tick, hipStream_t st) {
   return hipGetLastError();
 }
 
+// ---------------------------------------------------------------- LayerNorm fold: per-step u / v vectors
+// (kernels.h LnFoldArgs). Block = (layer, 64 output columns of W1 or Wqkv); thread = (column n = t & 63, step quarter
+// sq = t >> 6) accumulating u and v of 4 steps in fp32. Per K chunk of 64: the W chunk transposed into LDS as fp32
+// ([k][n], conflict-free reads across n), the 16 steps' scale/shift values of the chunk in LDS (one address per
+// wave: broadcast reads).
+template <typename T>
+__global__ __launch_bounds__(256) void lnfold_uv_kernel(LnFoldArgs a) {
+  __shared__ float Ws[64][65];
+  __shared__ float As[16][2][64];
+  const int t = threadIdx.x, n = t & 63, sq = t >> 6;
+  const int d = a.d, F = a.F, nbF = F / 64, nbQ = 3 * d / 64, nb = nbF + nbQ;
+  const int l = blockIdx.x / nb, j = blockIdx.x % nb;
+  const bool ff = j < nbF;
+  const int n0 = (ff ? j : j - nbF) * 64;
+  const T* W = reinterpret_cast<const T*>(ff ? a.w1[l] : a.wqkv[l]);
+  // AdaLN row layout per layer (modules.py:321-323): shift_msa, scale_msa, gate_msa, shift_mlp, scale_mlp, gate_mlp
+  const int64_t sh_off = (int64_t)l * 6 * d + (ff ? 3 : 0) * d, sc_off = sh_off + d;
+  const int64_t LW = 2 * (int64_t)F + 6 * (int64_t)d;
+  const int64_t u_off = a.out_off + l * LW + (ff ? 0 : 2 * (int64_t)F), v_off = u_off + (ff ? F : 3 * d);
+  for (int s0 = 0; s0 < a.nfe; s0 += 16) {
+    float au[4] = {0.f, 0.f, 0.f, 0.f}, av[4] = {0.f, 0.f, 0.f, 0.f};
+    for (int k0 = 0; k0 < d; k0 += 64) {
+      __syncthreads();
+      {  // W rows n0 .. n0+63, columns k0 .. k0+63: thread t takes row t >> 2, 16 columns
+        const int r = t >> 2, kq = (t & 3) * 16;
+        const T* src = W + (int64_t)(n0 + r) * d + k0 + kq;
+#pragma unroll
+        for (int e = 0; e < 16; ++e) Ws[kq + e][r] = to_f32(src[e]);
+      }
+      {  // scale / shift of steps s0 .. s0+15 over the chunk: thread t takes step t >> 4, one of the two, 8 values
+        const int sl = t >> 4, which = (t >> 3) & 1, kq = (t & 7) * 8, s = s0 + sl;
+        const float* src = a.table + (int64_t)min(s, a.nfe - 1) * a.stride + (which ? sh_off : sc_off) + k0 + kq;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) As[sl][which][kq + e] = src[e];
+      }
+      __syncthreads();
+#pragma unroll 8
+      for (int k = 0; k < 64; ++k) {
+        const float w = Ws[k][n];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          au[q] += (1.f + As[sq * 4 + q][0][k]) * w;
+          av[q] += As[sq * 4 + q][1][k] * w;
+        }
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int s = s0 + sq * 4 + q;
+      if (s < a.nfe) {
+        a.table[(int64_t)s * a.stride + u_off + n0 + n] = au[q];
+        a.table[(int64_t)s * a.stride + v_off + n0 + n] = av[q];
+      }
+    }
+  }
+}
+hipError_t lnfold_uv(int compute, const LnFoldArgs& a, hipStream_t st) {
+  if (a.d % 64 || a.F % 64 || a.nfe <= 0 || a.depth <= 0) return hipErrorInvalidValue;
+  const dim3 grid(a.depth * (a.F / 64 + 3 * a.d / 64)), block(256);
+  if (compute == F5H_C_BF16)
+    hipLaunchKernelGGL(lnfold_uv_kernel<bf16>, grid, block, 0, st, a);
+  else if (compute == F5H_C_FP16)
+    hipLaunchKernelGGL(lnfold_uv_kernel<f16>, grid, block, 0, st, a);
+  else
+    return hipErrorInvalidValue;
+  return hipGetLastError();
+}
+
 // p[0..n) = 0 by vector stores (the phase chain's arrival counters, zeroed ahead of every step)
 __global__ void zero_words_kernel(uint4* p, int64_t n4) {
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (int64_t)gridDim.x * blockDim.x)

@@ -70,13 +70,13 @@ struct Layer {
 struct GraphKey {
   const void* ws;
   int kind;  // 0: one NFE step, 1: the call prologue (inputs staged into the workspace)
-  int B, N, nt, nfe, use_cfg, batch_mask, probe, split, pad_skip, chain;
+  int B, N, nt, nfe, use_cfg, batch_mask, probe, split, pad_skip, chain, lnfold;
   uint64_t kernel_epoch;  // bumped whenever a forced GEMM config changes
   uint32_t cfg_bits;
   bool operator==(const GraphKey& o) const {
     return ws == o.ws && kind == o.kind && B == o.B && N == o.N && nt == o.nt && nfe == o.nfe && kernel_epoch == o.kernel_epoch &&
            use_cfg == o.use_cfg && batch_mask == o.batch_mask && probe == o.probe && cfg_bits == o.cfg_bits &&
-           split == o.split && pad_skip == o.pad_skip && chain == o.chain;
+           split == o.split && pad_skip == o.pad_skip && chain == o.chain && lnfold == o.lnfold;
   }
 };
 
@@ -125,6 +125,16 @@ struct f5h_engine {
   // re-zeroed on every graph replay it measured C2 58.4 vs 51.1 ms unchained (profiles/r06_ab_chain_c2.txt); the
   // round-5 gain came from a captured memset node that later replays did not apply (waits skipped, wrong results).
   int chain = 0;
+  // LayerNorm fold (DESIGN.md §3 'LayerNorm fold'): on the 16-bit DiT path without row masks the AdaLN LayerNorms
+  // between the residual GEMMs and their consumers run as algebra in those GEMMs (gemm_impl.h LNF) instead of as
+  // launches of their own. f5h_set_ln_fold, env F5H_LNFOLD=0 at creation turns it off. lnf_ok: the engine supports
+  // it (DiT, 16-bit, dim and ff a multiple of 64, dim <= 1024); lnf_w: device array [W1 of every layer, Wqkv of every
+  // layer] for lnfold_uv; ada_row: floats per AdaLN table row (the modulation rows, then per layer the fold's u/v).
+  int lnfold = 1;
+  bool lnf_ok = false;
+  const void** lnf_w = nullptr;
+  int64_t ada_row = 0;
+  std::atomic<int64_t> n_lnfold{0};  // backbone passes enqueued with the fold
   // The chain's give-up word (chain.h): device memory of the engine, set by a chain wait that expired. The call's final
   // kernel then writes NaN results; a copy of it lands in a pinned host word (fault_host) at the end of every chained
   // call, and the engine's next call reads that word, fails with F5H_EHIP and switches the chain off.
@@ -478,6 +488,7 @@ struct Bufs {
   float2* rope;
   uint8_t* rowkeep;
   int32_t* kvlen;
+  float* lnp;          // LayerNorm fold partial statistics [rows][d / 64][2]
   unsigned* chain;     // phase-chain arrival counters: [depth][5][chain_g4] (the chain runs on the packed batch only)
   int chain_g4;        // row groups per counter row, rounded up to 4 (16-B rows)
   float *ada_cur, *temb_cur, *tgrid;  // the current step's table rows; device copy of the grid
@@ -506,7 +517,7 @@ static void layout(const f5h_engine* e, WS& ws, Bufs& b, int B, int N, int nfe, 
   b.th = ws.take<float>((size_t)nfe * d);
   b.temb = ws.take<float>((size_t)nfe * d);
   b.tin_op = ws.take<char>((size_t)nfe * std::max(256, d) * es);
-  b.ada = a.backbone == F5H_DIT ? ws.take<float>((size_t)nfe * e->ada.Npad) : nullptr;
+  b.ada = a.backbone == F5H_DIT ? ws.take<float>((size_t)nfe * e->ada_row) : nullptr;
   b.te = ws.take<float>((size_t)2 * B * N * td);
   b.keepfill = ws.take<uint8_t>((size_t)2 * B * N);
   if (a.conv_layers > 0) {
@@ -536,7 +547,9 @@ static void layout(const f5h_engine* e, WS& ws, Bufs& b, int B, int N, int nfe, 
   b.kvlen = ws.take<int32_t>(S);
   b.chain_g4 = ((int)((rows + kChainRows - 1) / kChainRows) + 3) / 4 * 4;
   b.chain = a.backbone == F5H_DIT ? ws.take<unsigned>((size_t)a.depth * 5 * b.chain_g4) : nullptr;
-  b.ada_cur = a.backbone == F5H_DIT ? ws.take<float>((size_t)e->ada.Npad) : nullptr;
+  b.ada_cur = a.backbone == F5H_DIT ? ws.take<float>((size_t)e->ada_row) : nullptr;
+  // LayerNorm fold: per row and 64-column strip of the residual stream, (mean, M2) (float2)
+  b.lnp = e->lnf_ok ? ws.take<float>(rows * (size_t)(d / 64) * 2) : nullptr;
   b.temb_cur = ws.take<float>((size_t)d);
   b.tgrid = ws.take<float>((size_t)nfe);
   b.kstep = ws.take<int>(64);
@@ -594,6 +607,7 @@ struct Ctx {
   hipStream_t st2;            // second stream for the unconditional branch (step-graph capture), or null
   int site;  // probe launch-site counter, reset at the start of every step's enqueue
   int chain;  // this call may run the phase chain (engine switch, shape, and chain_admit's per-device check)
+  int lnfold;  // this call runs the LayerNorm fold (engine switch, shape; never beside the chain)
   double* hp;  // host milliseconds of the call by phase (kHostPhases, f5h_last_call_host_ms), or null
 };
 // Host time of an f5h_sample call by phase (f5h_last_call_host_ms): a call that blocks the host shows where.
@@ -652,8 +666,21 @@ static int prologue(Ctx& c, const float* t_host, int nt_vals, const float* cond,
     KCK(gemm(bf, EPI_STORE, g, st));
     if (a.backbone == F5H_DIT) {
       KCK(silu_to_op(bf, b.temb, b.tin_op, (int64_t)nt_vals * d, st));
-      g = gargs(b.tin_op, d, e->ada, nt_vals, b.ada, e->ada.Npad);
+      g = gargs(b.tin_op, d, e->ada, nt_vals, b.ada, e->ada_row);
       KCK(gemm(bf, EPI_STORE, g, st));
+      if (c.lnfold) {  // every step's u / v of the folded LayerNorms (kernels.h LnFoldArgs)
+        LnFoldArgs la{};
+        la.table = b.ada;
+        la.stride = e->ada_row;
+        la.out_off = e->ada.Npad;
+        la.nfe = nt_vals;
+        la.depth = a.depth;
+        la.d = d;
+        la.F = a.ff_dim;
+        la.w1 = e->lnf_w;
+        la.wqkv = e->lnf_w + a.depth;
+        KCK(lnfold_uv(bf, la, st));
+      }
     }
   }
   // ---- text embedding, both branches (cached once per call in the reference, dit.py:294-310);
@@ -700,7 +727,7 @@ constexpr int kArrive = 16;
 static int step_prep(Ctx& c) {
   f5h_engine* e = c.e;
   if (e->a.backbone == F5H_DIT)
-    KCK(step_begin(c.b.kstep, c.b.ada, e->ada.Npad, e->ada.Npad, c.b.ada_cur, c.st));
+    KCK(step_begin(c.b.kstep, c.b.ada, e->ada_row, e->ada_row, c.b.ada_cur, c.st));
   else
     KCK(step_begin(c.b.kstep, c.b.temb, e->a.dim, e->a.dim, c.b.temb_cur, c.st));
   return 0;
@@ -822,6 +849,25 @@ static int backbone_part(Ctx& c, int s0, int ns, hipStream_t st) {
   }
   bool qkv_done = false;    // this layer's LayerNorm + QKV came with the previous layer's chain
   bool final_done = false;  // the final LayerNorm came with the last layer's chain
+  // LayerNorm fold (engine.lnfold): the attention-norm of layers 1.. and every FFN-norm run inside the GEMMs around
+  // them; the first layer's attention-norm and the final norm stay launches. lnf(l): layer l's u/v block of the
+  // current step's table row (kernels.h LnFoldArgs layout)
+  const bool fold_on = c.lnfold && dit && r16 && do_ln && !keep && !chain_on && b.lnp && e->lnf_ok;
+  const int64_t lnf_lw = 2 * (int64_t)a.ff_dim + 6 * (int64_t)d;
+  auto lnf = [&](int l) { return ada_k + e->ada.Npad + (int64_t)l * lnf_lw; };
+  auto fold_consumer = [&](GemmArgs& g, const float* u, const float* v) {
+    g.ln_part_in = b.lnp + ro * (size_t)(d / 64) * 2;
+    g.ln_nparts = d / 64;
+    g.ln_u = u;
+    g.ln_v = v;
+  };
+  auto fold_producer = [&](GemmArgs& g, const float* scale) {
+    g.hs = aop;
+    g.hs_scale = scale;
+    g.ln_part = b.lnp + ro * (size_t)(d / 64) * 2;
+    g.ln_nparts = d / 64;
+  };
+  if (fold_on) e->n_lnfold.fetch_add(1, std::memory_order_relaxed);
   for (int l = 0; l < a.depth; ++l) {
     Layer& Ly = e->layers[l];
     const float* ad = ada_k ? ada_k + (size_t)l * 6 * d : nullptr;
@@ -846,10 +892,12 @@ static int backbone_part(Ctx& c, int s0, int ns, hipStream_t st) {
         KCK(rms_norm_g(bf, h, r16, rows, d, Ly.g_attn, aop, st));
       }
     } else {
-      if (do_ln && !qkv_done) KCK(ln_modulate(bf, h, r16, rows, d, ad /*shift_msa*/, ad + d /*scale_msa*/, aop, st));
+      if (do_ln && !qkv_done && !(fold_on && l > 0))
+        KCK(ln_modulate(bf, h, r16, rows, d, ad /*shift_msa*/, ad + d /*scale_msa*/, aop, st));
     }
     if (!qkv_done) {
       GemmArgs g = qkv_args(Ly);
+      if (fold_on && l > 0) fold_consumer(g, lnf(l) + 2 * a.ff_dim, lnf(l) + 2 * a.ff_dim + 3 * d);
       ProbeScope ps(e, KC_QKV, st, &c.site, &g.probe);
       KCK(gemm(bf, EPI_QKV, g, st));
     }
@@ -911,10 +959,11 @@ static int backbone_part(Ctx& c, int s0, int ns, hipStream_t st) {
         g.live_len = b.kvlen + s0;
         g.live_seq = c.L;
       }
+      if (fold_on) fold_producer(g, ad + 4 * d /*scale_mlp: hs = h (1 + scale_mlp) for FFN1*/);
       ProbeScope ps(e, KC_OUT, st, &c.site, &g.probe);
       KCK(gemm(bf, epi_resid, g, st));
     }
-    {
+    if (!fold_on) {
       ProbeScope ps(e, KC_NORM, st, &c.site);
       if (dit) {
         if (do_ln) KCK(ln_modulate(bf, h, r16, rows, d, ad + 3 * d /*shift_mlp*/, ad + 4 * d /*scale_mlp*/, aop, st));
@@ -924,12 +973,15 @@ static int backbone_part(Ctx& c, int s0, int ns, hipStream_t st) {
     }
     {
       GemmArgs g = gargs(aop, d, Ly.ff1, rows, f, a.ff_dim);
+      if (fold_on) fold_consumer(g, lnf(l), lnf(l) + a.ff_dim);
       ProbeScope ps(e, KC_FFN1, st, &c.site, &g.probe);
       KCK(gemm(bf, EPI_GELU_TANH, g, st));
     }
     {
       GemmArgs g = gargs(f, a.ff_dim, Ly.ff2, rows, h, d);
       g.gate = ad ? ad + 5 * d : nullptr;  // gate_mlp
+      // the next layer's attention-norm: hs = h (1 + scale_msa of layer l + 1) for its QKV
+      if (fold_on && l + 1 < a.depth) fold_producer(g, ada_k + (size_t)(l + 1) * 6 * d + d);
       ProbeScope ps(e, KC_FFN2, st, &c.site, &g.probe);
       KCK(gemm(bf, epi_resid, g, st));
     }
@@ -1189,6 +1241,18 @@ int f5h_engine_create_views(const f5h_arch* arch, const f5h_tensor_view* weights
     W.m[v.name] = WView{dp, v.dtype, v.numel};
   }
   if (!rc) rc = pack_all(e, W);
+  // LayerNorm fold support and the AdaLN table row length (DiT: the modulation rows, then the fold's u/v per layer)
+  if (!rc && arch->backbone == F5H_DIT) {
+    e->lnf_ok = e->bf != 0 && arch->dim % 64 == 0 && arch->dim <= 1024 && arch->ff_dim % 64 == 0;
+    e->ada_row = e->ada.Npad + (e->lnf_ok ? (int64_t)arch->depth * (2 * (int64_t)arch->ff_dim + 6 * (int64_t)arch->dim) : 0);
+    if (e->lnf_ok) {
+      std::vector<const void*> wp;
+      for (const Layer& L : e->layers) wp.push_back(L.ff1.w);
+      for (const Layer& L : e->layers) wp.push_back(L.qkv.w);
+      if (upload(e, wp, &e->lnf_w)) e->lnf_ok = false;
+    }
+  }
+  if (const char* lv = getenv("F5H_LNFOLD")) e->lnfold = (*lv == '0') ? 0 : 1;
   // packing ran on the engine's stream (no device-wide synchronisation)
   if (!rc && hipStreamSynchronize(e->mstream) != hipSuccess) rc = fail(F5H_EHIP, "weight packing");
   for (void* t : staged) dev_free(t, e->mstream);
@@ -1308,6 +1372,7 @@ static GraphKey prologue_key(const Ctx& c, const void* ws) {
   key.nfe = c.nfe;
   key.use_cfg = c.use_cfg;
   key.batch_mask = c.batch_mask;
+  key.lnfold = c.lnfold;
   key.kernel_epoch = g_kernel_epoch.load();
   return key;
 }
@@ -1352,6 +1417,7 @@ int f5h_sample(f5h_engine* e, void* stream, const f5h_sample_args* a, void* work
   RC(chain_fault_check(e, c.st));
   ChainTicket ticket;  // (declared after `used`: its event is recorded first, both after every launch of the call)
   c.chain = chain_for_call(e, c, ticket);
+  c.lnfold = e->lnfold && e->lnf_ok && !c.batch_mask && !c.chain;
   double hp[kHostPhases] = {};
   c.hp = hp;
   const double h0 = host_ms();
@@ -1424,8 +1490,8 @@ static int enqueue_step(Ctx& c, const f5h_sample_args* a) {
     u.trajp = c.b.trajp;
     const bool dit = e->a.backbone == F5H_DIT;
     u.next_src = dit ? c.b.ada : c.b.temb;
-    u.next_stride = dit ? e->ada.Npad : e->a.dim;
-    u.next_n = dit ? (int)e->ada.Npad : e->a.dim;
+    u.next_stride = dit ? e->ada_row : e->a.dim;
+    u.next_n = dit ? (int)e->ada_row : e->a.dim;
     u.next_dst = dit ? c.b.ada_cur : c.b.temb_cur;
     u.nfe = c.nfe;
     u.arrive = reinterpret_cast<unsigned*>(c.b.kstep + kArrive);
@@ -1454,6 +1520,7 @@ static int run_steps(Ctx& c, const f5h_sample_args* a, const void* ws) {
   key.split = split;
   key.pad_skip = e->pad_skip;
   key.chain = c.chain;
+  key.lnfold = c.lnfold;
   key.kernel_epoch = g_kernel_epoch.load();
   std::memcpy(&key.cfg_bits, &a->cfg_strength, 4);
   std::shared_ptr<GraphEntry> hold;  // keeps the replayed graph alive through the launch loop
@@ -1643,6 +1710,7 @@ int f5h_forward(f5h_engine* e, void* stream, const f5h_forward_args* a, void* wo
   RC(chain_fault_check(e, c.st));
   ChainTicket ticket;
   c.chain = chain_for_call(e, c, ticket);
+  c.lnfold = e->lnfold && e->lnf_ok && !c.batch_mask && !c.chain;
   const bool cached = a->text_cache == 2;
   if (a->t_dev) {  // time read on the stream: no host round trip (dit.py:332-333 takes a tensor)
     HIPCK(hipMemcpyAsync(c.b.tgrid, a->t_dev, sizeof(float), hipMemcpyDeviceToDevice, c.st));
@@ -1675,6 +1743,7 @@ int f5h_forward(f5h_engine* e, void* stream, const f5h_forward_args* a, void* wo
     key.probe = e->probe_class;
     key.pad_skip = e->pad_skip;
     key.chain = c.chain;
+    key.lnfold = c.lnfold;
     key.kernel_epoch = g_kernel_epoch.load();
     std::shared_ptr<GraphEntry> hold;
     RC(graph_get(c, key, false, body, hold, 1));
@@ -1794,6 +1863,21 @@ int f5h_chain_stats(f5h_engine* e, int64_t* launches, int32_t* fault, int64_t* r
       *fault = v ? 1 : 0;
     }
   }
+  return 0;
+}
+
+int f5h_set_ln_fold(f5h_engine* e, int32_t enable) {
+  if (!e) return fail(F5H_EINVAL, "null engine");
+  if (enable != 0 && enable != 1) return fail(F5H_EINVAL, "ln fold must be 0 or 1");
+  std::lock_guard<std::mutex> g(e->gm);
+  e->lnfold = enable;
+  return 0;
+}
+
+int f5h_ln_fold_stats(f5h_engine* e, int32_t* supported, int64_t* passes) {
+  if (!e) return fail(F5H_EINVAL, "null engine");
+  if (supported) *supported = e->lnf_ok ? 1 : 0;
+  if (passes) *passes = e->n_lnfold.load(std::memory_order_relaxed);
   return 0;
 }
 

@@ -306,6 +306,31 @@ F5H_DEV void store8_rs(__amdgpu_buffer_rsrc_t r, uint32_t elem, const V8& x) {
   }
 }
 
+// ---- LayerNorm fold helpers (GemmArgs hs / ln_part_in; DESIGN.md §3 'LayerNorm fold')
+typedef unsigned u32x2_t __attribute__((ext_vector_type(2)));
+// DPP move inside each group of 8 consecutive lanes (the 8 lanes holding one 64-column row segment in the strip
+// epilogue): quad_perm xor 1, quad_perm xor 2, row_half_mirror
+template <int CTRL>
+F5H_DEV float dpp8(float x) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), CTRL, 0xF, 0xF, false));
+}
+F5H_DEV float sum8(float v) {
+  v += dpp8<0xB1>(v);
+  v += dpp8<0x4E>(v);
+  return v + dpp8<0x141>(v);
+}
+// Chan's pairwise combination of (count, mean, M2) partial statistics: (n, m, q) <- (n, m, q) + (nb, mb, qb)
+F5H_DEV void chan_add(float& n, float& m, float& q, float nb, float mb, float qb) {
+  const float nt = n + nb, f = nt > 0.f ? nb / nt : 0.f, dl = mb - m;
+  q = q + qb + dl * dl * n * f;
+  m = m + dl * f;
+  n = nt;
+}
+template <int CTRL>
+F5H_DEV void chan_dpp(float& n, float& m, float& q) {
+  chan_add(n, m, q, dpp8<CTRL>(n), dpp8<CTRL>(m), dpp8<CTRL>(q));
+}
+
 // Fast epilogue of one wave's sub-tile (whole-column tiles of the hot epilogues), per 16-row strip:
 // accumulators -> the wave's LDS strip (fp32, EPAD-float rows; one ds_write_b128 per block, the swapped-operand
 // layout holding four consecutive columns per lane) -> 8-column chunks of whole rows, so that every store
@@ -322,18 +347,43 @@ F5H_DEV void store8_rs(__amdgpu_buffer_rsrc_t r, uint32_t elem, const V8& x) {
 // Shared by gemm_kernel and gemm_pp_kernel.
 // PD: strips of row data fetched ahead (1: the next strip's; fetching every strip's residual up front in the 256x256
 // ping-pong kernel measured equal at C4/C5, profiles/r05_ab_c4_c5_resid_prefetch.txt)
+// LNF (LayerNorm fold): 0 none, 1 producer (EPI_RESID16: also hs and the row-strip statistics), 2 consumer
+// (EPI_GELU_TANH / EPI_QKV: the normalisation applied to the accumulators); see GemmArgs.
 template <typename TC, int EPI, int MT, int NT, int WN, int EPAD, bool PREF, bool BIAS, int PM, int PT, int AUX = 0,
-          int PD = 1>
+          int PD = 1, int LNF = 0>
 F5H_DEV void epilogue_fast_t(const GemmArgs& g, const f32x4 (&acc)[MT][NT], float* Cs, int rbase, int cbase,
                              int lane, const V8 (&pre)[PM][PT]) {
   constexpr int CH = WN / 8;          // 8-column chunks per strip row
   constexpr int TPC = 16 * CH / 64;   // chunks per lane per strip
   static_assert(64 % CH == 0 && (16 * CH) % 64 == 0, "whole chunks per lane");
+  static_assert(LNF == 0 || (WN == 64 && is16<TC>()), "the LayerNorm fold: 64-column wave strips, 16-bit operands");
+  static_assert(LNF != 1 || EPI == EPI_RESID16, "fold producer: the 16-bit residual epilogue");
+  static_assert(LNF != 2 || EPI == EPI_GELU_TANH || EPI == EPI_QKV, "fold consumer: FFN1 or QKV");
   const int fr = lane & 15, q = lane >> 4;
   const int cc = lane % CH;
   const int col = cbase + cc * 8;
   V8 bias8 = V8{};
   if constexpr (BIAS) bias8 = load8(g.bias + col);
+  // LayerNorm fold: producer's (1 + scale) of its columns, hs / statistics destinations, its 64-column strip; the
+  // consumer's ln_u / ln_v of its columns and the partial-statistics source
+  V8 lnA = V8{}, lnB = V8{};
+  __amdgpu_buffer_rsrc_t ln_dst = rsrc_of(nullptr, 0), ln_st = rsrc_of(nullptr, 0);
+  int ln_p = 0;
+  const int ln_np = g.ln_nparts;
+  if constexpr (LNF == 1) {
+    lnA = load8(g.hs_scale + col);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) lnA.v[e] = 1.f + lnA.v[e];
+    ln_dst = rsrc_of(g.hs, (uint64_t)g.M * g.ldc * sizeof(TC));
+    ln_st = rsrc_of(g.ln_part, (uint64_t)g.M * ln_np * 8);
+    ln_p = __builtin_amdgcn_readfirstlane(cbase >> 6);
+  } else if constexpr (LNF == 2) {
+    lnA = load8(g.ln_u + col);
+    lnB = load8(g.ln_v + col);
+    ln_st = rsrc_of(g.ln_part_in, (uint64_t)g.M * ln_np * 8);
+  }
+  const int lp0 = min(cc, ln_np - 1), lp1 = min(cc + 8, ln_np - 1);  // this lane's two partials (consumer)
+  const float ln_n0 = cc < ln_np ? 64.f : 0.f, ln_n1 = cc + 8 < ln_np ? 64.f : 0.f;
   V8 gate8 = V8{{1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f}};
   if constexpr (EPI == EPI_RESID || EPI == EPI_RESID16)
     if (g.gate) gate8 = load8(g.gate + col);
@@ -363,6 +413,7 @@ F5H_DEV void epilogue_fast_t(const GemmArgs& g, const f32x4 (&acc)[MT][NT], floa
     u32x4 d0, d1;  // RoPE (cos, sin) of four pairs (QKV, fp32), the residual row chunk (RESID), the addend (INPROJ)
     u32x4 e0, e1;  // INPROJ: the second output row's addend
     uint32_t kb;   // RESID row-mask byte
+    u32x2_t s0, s1;  // LayerNorm fold consumer: two (mean, M2) partials of the row
   };
   const __amdgpu_buffer_rsrc_t rk = rsrc_of(g.rowkeep, g.rowkeep ? (uint64_t)g.M : 0);  // null: reads 0
   const bool masked = g.rowkeep != nullptr;
@@ -390,6 +441,10 @@ F5H_DEV void epilogue_fast_t(const GemmArgs& g, const f32x4 (&acc)[MT][NT], floa
     for (int t = 0; t < TPC; ++t) {
       const int rr = t * (64 / CH) + lane / CH;
       const int rowc = min(rbase + i * 16 + rr, g.M - 1);
+      if constexpr (LNF == 2) {
+        ri[t].s0 = __builtin_amdgcn_raw_buffer_load_b64(ln_st, (uint32_t)((rowc * ln_np + lp0) * 8), 0, 0);
+        ri[t].s1 = __builtin_amdgcn_raw_buffer_load_b64(ln_st, (uint32_t)((rowc * ln_np + lp1) * 8), 0, 0);
+      }
       if constexpr (EPI == EPI_QKV) {
         (void)rowc;
         const u32x4* p = reinterpret_cast<const u32x4*>(g.rope + pf_pos[t] * 32 + (dh >> 1));
@@ -446,11 +501,22 @@ F5H_DEV void epilogue_fast_t(const GemmArgs& g, const f32x4 (&acc)[MT][NT], floa
       const float* src = Cs + rr * EPAD + cc * 8;
       const float4 a0 = *reinterpret_cast<const float4*>(src), a1 = *reinterpret_cast<const float4*>(src + 4);
       V8 x{{a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w}};
+      const RowIn& ri = rbuf[i % RB][t];
+      if constexpr (LNF == 2) {
+        // the row's statistics from its strips' partials: two per lane, then across the row's 8 lanes
+        float n = ln_n0, m = __uint_as_float(ri.s0.x), qq = __uint_as_float(ri.s0.y);
+        chan_add(n, m, qq, ln_n1, __uint_as_float(ri.s1.x), __uint_as_float(ri.s1.y));
+        chan_dpp<0xB1>(n, m, qq);
+        chan_dpp<0x4E>(n, m, qq);
+        chan_dpp<0x141>(n, m, qq);
+        const float rstd = rsqrtf(qq / n + 1e-6f);  // LayerNorm eps 1e-6 (modules.py:316,336)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) x.v[e] = rstd * (x.v[e] - m * lnA.v[e]) + lnB.v[e];
+      }
       if constexpr (BIAS) {
 #pragma unroll
         for (int e = 0; e < 8; ++e) x.v[e] = add_nc(x.v[e], bias8.v[e]);
       }
-      const RowIn& ri = rbuf[i % RB][t];
       if constexpr (EPI == EPI_QKV) {
         const V8 cs = as_v8(ri);
         // interleaved pairs (a, b) -> (a c - b s, b c + a s) as packed products and one packed add (each
@@ -483,6 +549,27 @@ F5H_DEV void epilogue_fast_t(const GemmArgs& g, const f32x4 (&acc)[MT][NT], floa
 #pragma unroll
         for (int e = 0; e < 8; ++e) o.v[e] = resid_add(c.v[e], gate8.v[e], x.v[e], keep);
         store8_rs<ResT<TC, EPI>, AUX>(dst, (uint32_t)((int64_t)row * g.ldc + col), o);
+        if constexpr (LNF == 1) {
+          // the stored (rounded) h values: hs = h (1 + scale) for the consumer, and this 64-column strip's
+          // (mean, M2) of h (two passes over the row's 8 lanes)
+          V8 hr, hv;
+          float sm = 0.f;
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            hr.v[e] = to_f32(from_f32<TC>(o.v[e]));
+            hv.v[e] = hr.v[e] * lnA.v[e];
+            sm += hr.v[e];
+          }
+          store8_rs<TC, AUX>(ln_dst, (uint32_t)((int64_t)row * g.ldc + col), hv);
+          const float mean = sum8(sm) * (1.f / 64.f);
+          float m2 = 0.f;
+#pragma unroll
+          for (int e = 0; e < 8; ++e) m2 += (hr.v[e] - mean) * (hr.v[e] - mean);
+          m2 = sum8(m2);
+          // the row's 8 lanes store the same 8 bytes (no branch); rows >= M fall outside the descriptor
+          __builtin_amdgcn_raw_buffer_store_b64(u32x2_t{__float_as_uint(mean), __float_as_uint(m2)}, ln_st,
+                                                (uint32_t)((row * ln_np + ln_p) * 8), 0, AUX);
+        }
       } else if constexpr (EPI == EPI_GELU_TANH || EPI == EPI_GELU_ERF_OP) {
         if constexpr (EPI == EPI_GELU_TANH && is16<TC>()) {
 #pragma unroll
@@ -526,6 +613,26 @@ F5H_DEV void epilogue_fast_t(const GemmArgs& g, const f32x4 (&acc)[MT][NT], floa
 template <typename TC, int EPI, int MT, int NT, int WN, int EPAD, bool PREF, int AUX = 0, int PD = 1, int PM, int PT>
 F5H_DEV void epilogue_fast(const GemmArgs& g, const f32x4 (&acc)[MT][NT], float* Cs, int rbase, int cbase,
                            int lane, const V8 (&pre)[PM][PT]) {
+  // LayerNorm fold forms (GemmArgs hs / ln_part_in: 16-bit, 64-column wave strips; bias always present there)
+  if constexpr (WN == 64 && is16<TC>() && AUX == 0) {
+    if constexpr (EPI == EPI_RESID16) {
+      if (g.hs) {
+        if (g.bias)
+          epilogue_fast_t<TC, EPI, MT, NT, WN, EPAD, PREF, true, PM, PT, AUX, PD, 1>(g, acc, Cs, rbase, cbase, lane, pre);
+        else
+          epilogue_fast_t<TC, EPI, MT, NT, WN, EPAD, PREF, false, PM, PT, AUX, PD, 1>(g, acc, Cs, rbase, cbase, lane, pre);
+        return;
+      }
+    } else if constexpr (EPI == EPI_GELU_TANH || EPI == EPI_QKV) {
+      if (g.ln_part_in) {
+        if (g.bias)
+          epilogue_fast_t<TC, EPI, MT, NT, WN, EPAD, PREF, true, PM, PT, AUX, PD, 2>(g, acc, Cs, rbase, cbase, lane, pre);
+        else
+          epilogue_fast_t<TC, EPI, MT, NT, WN, EPAD, PREF, false, PM, PT, AUX, PD, 2>(g, acc, Cs, rbase, cbase, lane, pre);
+        return;
+      }
+    }
+  }
   if (g.bias)
     epilogue_fast_t<TC, EPI, MT, NT, WN, EPAD, PREF, true, PM, PT, AUX, PD>(g, acc, Cs, rbase, cbase, lane, pre);
   else
@@ -1782,6 +1889,16 @@ static hipError_t launch_t(const GemmArgs& a, hipStream_t st) {
   if (a.M == 0) return hipSuccess;
   int cfg = 0;
   if constexpr (is16<TC>()) cfg = gemm_select_cfg(a);
+  // the LayerNorm fold runs only in the strip epilogue of the 64-column-strip configurations (0, 1, 5, 11): refuse
+  // it anywhere else rather than ignore it (the results would be those of an unnormalised operand)
+  if (a.hs || a.ln_part_in) {
+    const bool prod = a.hs && EPI == EPI_RESID16 && a.hs_scale && a.ln_part;
+    const bool cons = a.ln_part_in && (EPI == EPI_GELU_TANH || EPI == EPI_QKV) && a.ln_u && a.ln_v;
+    const int bn = cfg == 11 ? 256 : 128;
+    if (!is16<TC>() || (a.hs && a.ln_part_in) || !(prod || cons) || a.ln_nparts <= 0 || a.ln_nparts > 16 ||
+        (cfg != 0 && cfg != 1 && cfg != 5 && cfg != 11) || !fast_epi_ok<EPI>(a, bn) || a.rowkeep || a.live_len)
+      return hipErrorInvalidValue;
+  }
   switch (cfg) {
     case 0: launch_cfg<TC, EPI, 64, 128, 2, 2, 3>(a, st); break;
     case 1: launch_cfg<TC, EPI, 128, 128, 2, 2, 2>(a, st); break;

@@ -66,6 +66,16 @@ struct GemmArgs {
   // the masked rows of a computed tile do). Null: every tile is computed.
   const int32_t* live_len; int live_seq;
   int group_m;                     // persistent kernel (cfg 13): tile order in groups of this many row tiles (<= 1: n-fastest)
+  // LayerNorm fold (DiT 16-bit path without row masks; DESIGN.md §3 'LayerNorm fold'). The AdaLN LayerNorm between a
+  // residual GEMM and its consumer, aop = LN(h) (1 + sc) + sh (modules.py:325,753), runs as algebra in the two GEMMs:
+  // producer (EPI_RESID16, hs != null): besides h, writes hs = round(h' (1 + hs_scale[n])) (h' = the stored, rounded
+  //   h; operand dtype, row stride ldc) and, per row and 64-column strip p, the strip's (mean, M2) of h' into
+  //   ln_part[row * ln_nparts + p] (float2; ln_nparts = N / 64);
+  // consumer (EPI_GELU_TANH / EPI_QKV, ln_part_in != null; A = hs): combines the row's ln_nparts partials into
+  //   (mean_m, rstd_m) and applies x = rstd_m (acc - mean_m ln_u[n]) + ln_v[n] before the bias, where
+  //   ln_u[n] = sum_k (1 + sc_k) W[n,k] and ln_v[n] = sum_k sh_k W[n,k] (lnfold_uv, per ODE step).
+  void* hs; const float* hs_scale; float* ln_part;
+  const float* ln_part_in; int ln_nparts; const float* ln_u; const float* ln_v;
 };
 
 // Does the row tile [m0, m0 + BM) of an M-row GEMM hold a live row? Sequence s (rows [s*live_seq, (s+1)*live_seq))
@@ -258,6 +268,18 @@ struct ChainArgs {
 inline size_t chain_counter_bytes(int M) {
   return (size_t)5 * ((M + kChainRows - 1) / kChainRows) * sizeof(unsigned);
 }
+// LayerNorm fold: out[s][l*LW + {0: u1, F: v1, 2F: u2, 2F+3d: v2} + n] (LW = 2F + 6d, rows of `stride` floats,
+// first column out_off) for every ODE step s < nfe and layer l < depth, with sc/sh the step's AdaLN rows of the
+// layer in table[s] (modulation layout of modules.py:321-323): FFN1 (W1 [F][d], mlp scale/shift) and QKV
+// (Wqkv [3d][d], msa scale/shift). u = sum_k (1 + sc_k) W[n,k], v = sum_k sh_k W[n,k], fp32.
+struct LnFoldArgs {
+  float* table; int64_t stride; int64_t out_off;
+  int nfe, depth, d, F;
+  const void* const* w1;    // [depth] device pointers (operand dtype [F][d])
+  const void* const* wqkv;  // [depth] device pointers (operand dtype [3d][d])
+};
+hipError_t lnfold_uv(int compute, const LnFoldArgs& a, hipStream_t st);
+
 // Launch the chain (16-bit operands, dim 1024, whole-column tiles); hipErrorInvalidValue when the shapes do not
 // fit it (the caller then issues the separate launches).
 hipError_t chain_launch(int compute, const ChainArgs& a, hipStream_t st);

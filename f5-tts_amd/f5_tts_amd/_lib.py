@@ -43,6 +43,8 @@ EXPORTS = (
     "f5h_set_chain",
     "f5h_chain_stats",
     "f5h_chain_debug_spin_limit",
+    "f5h_set_ln_fold",
+    "f5h_ln_fold_stats",
     "f5h_op_linear",
     "f5h_op_attention",
     "f5h_gemm_force_config",
@@ -173,6 +175,11 @@ def lib():
         L.f5h_set_chain.restype = ctypes.c_int
         L.f5h_chain_stats.argtypes = [vp, ctypes.POINTER(i64), ctypes.POINTER(i32), ctypes.POINTER(i64)]
         L.f5h_chain_stats.restype = ctypes.c_int
+    if hasattr(L, "f5h_set_ln_fold"):
+        L.f5h_set_ln_fold.argtypes = [vp, i32]
+        L.f5h_set_ln_fold.restype = ctypes.c_int
+        L.f5h_ln_fold_stats.argtypes = [vp, ctypes.POINTER(i32), ctypes.POINTER(i64)]
+        L.f5h_ln_fold_stats.restype = ctypes.c_int
     if hasattr(L, "f5h_chain_debug_spin_limit"):
         L.f5h_chain_debug_spin_limit.argtypes = [i64]
         L.f5h_chain_debug_spin_limit.restype = ctypes.c_int

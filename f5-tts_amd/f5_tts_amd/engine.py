@@ -131,6 +131,17 @@ class Engine:
         path without row masks; f5h_set_chain; default on). Results are bitwise identical either way."""
         _lib.check(_lib.lib().f5h_set_chain(self._h, int(bool(on))), "set_chain")
 
+    def set_ln_fold(self, on: bool):
+        """Run the AdaLN LayerNorms between the residual GEMMs and their consumers inside those GEMMs (16-bit DiT
+        path without row masks; f5h_set_ln_fold; default on). Not bitwise the separate launches."""
+        _lib.check(_lib.lib().f5h_set_ln_fold(self._h, int(bool(on))), "set_ln_fold")
+
+    def ln_fold_stats(self):
+        """(the engine can fold, backbone passes enqueued with the fold)."""
+        sup, n = ctypes.c_int32(), ctypes.c_int64()
+        _lib.check(_lib.lib().f5h_ln_fold_stats(self._h, ctypes.byref(sup), ctypes.byref(n)), "ln_fold_stats")
+        return bool(sup.value), int(n.value)
+
     def chain_stats(self):
         """(phase-chain launches this engine enqueued, 1 if one of its chain waits gave up and the engine has not
         reported it yet, chained calls of this process that the per-device concurrency rule sent to the separate

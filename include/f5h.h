@@ -226,6 +226,16 @@ int f5h_set_pad_skip(f5h_engine* eng, int32_t enable);
  * F5H_CHAIN=1 at creation: 1). Bitwise identical results; slower than the separate launches at C2 (58.4 vs
  * 51.1 ms), hence off. */
 int f5h_set_chain(f5h_engine* eng, int32_t enable);
+/* LayerNorm fold (DESIGN.md §3 'LayerNorm fold'): on the 16-bit DiT path without row masks, the AdaLN LayerNorm +
+ * modulate between a residual GEMM and its consumer (modules.py:325,753: out-proj -> FFN1, FFN2 -> the next QKV)
+ * runs inside those two GEMMs instead of as a launch of its own: the producer also writes h (1 + scale) and per-row
+ * (mean, M2) partials of h, the consumer normalises its accumulators, rstd (acc - mean u) + v with per-step vectors
+ * u = (1 + scale) W^T, v = shift W^T computed once per call. Not bitwise the separate launches (the statistics and
+ * the rounding point move): within the reduced-precision envelopes (tests/test_gpu_envelope.py). 1 (default) or 0
+ * (env F5H_LNFOLD=0 at creation: 0). f5h_ln_fold_stats: *supported = 1 when the engine can fold (DiT, 16-bit,
+ * dim and ff_dim multiples of 64, dim <= 1024), *passes = backbone passes enqueued with the fold. */
+int f5h_set_ln_fold(f5h_engine* eng, int32_t enable);
+int f5h_ln_fold_stats(f5h_engine* eng, int32_t* supported, int64_t* passes);
 /* Failure of the chain (never expected): a chain wait that gives up (a bounded spin of ~0.3 s) sets the
  * ENGINE's fault word; that call's `out` (f5h_sample) / `pred` (f5h_forward) is then all NaN, and the engine's
  * next f5h_sample / f5h_forward fails with F5H_EHIP (message in f5h_last_error), clears the word and turns the

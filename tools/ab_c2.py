@@ -4,7 +4,7 @@ arm's output is bitwise identical to the first arm's.
 
     python tools/ab_c2.py [--config c2] [--rounds 5] [--calls 5] [--arms streams1,streams2]
 Arms: streams1 / streams2 (f5h_set_cfg_streams), gemmN (f5h_gemm_force_config N, -1 = auto),
-eager (step graph off), chain0 / chain1 (f5h_set_chain). Outputs are compared for the warm call (a graph capture)
+eager (step graph off), chain0 / chain1 (f5h_set_chain), fold0 / fold1 (f5h_set_ln_fold). Outputs are compared for the warm call (a graph capture)
 AND the last timed call of every arm (graph replays only: round 6 found a bug that only replays showed).
 """
 import argparse
@@ -49,6 +49,8 @@ def main():
         gemm_force_config(int(arm[4:]) if arm.startswith("gemm") else -1)
         if arm.startswith("chain"):
             eng.set_chain(arm == "chain1")
+        if arm.startswith("fold"):
+            eng.set_ln_fold(arm == "fold1")
 
     outs, lasts, times = {}, {}, {arm: [] for arm in arms}
     for arm in arms:  # warm every arm (graph capture) before timing
@@ -70,8 +72,10 @@ def main():
     for arm in arms:
         t = sorted(times[arm])
         same = torch.equal(outs[arm], outs[arms[0]]) and torch.equal(lasts[arm], outs[arms[0]])
+        ref = outs[arms[0]].float()
+        rel = float((lasts[arm].float() - ref).norm() / ref.norm())
         print(f"{arm:10s} median {t[len(t) // 2]:8.3f} ms  min {t[0]:8.3f} ms  bitwise-equal-to-{arms[0]} {same} "
-              f"(warm and last timed call)", flush=True)
+              f"(warm and last timed call; rel-L2 of the last {rel:.3e})", flush=True)
 
 
 if __name__ == "__main__":
