@@ -121,64 +121,84 @@ hipError_t step_advance(int* kstep, int* tick, hipStream_t st) {
 }
 
 // ---------------------------------------------------------------- LayerNorm fold: per-step u / v vectors
-// (kernels.h LnFoldArgs). Block = (layer, 64 output columns of W1 or Wqkv); thread = (column n = t & 63, step quarter
-// sq = t >> 6) accumulating u and v of 4 steps in fp32. Per K chunk of 64: the W chunk transposed into LDS as fp32
-// ([k][n], conflict-free reads across n), the 16 steps' scale/shift values of the chunk in LDS (one address per
-// wave: broadcast reads).
+// (kernels.h LnFoldArgs). u_s[n] = sum_k (1 + scale_s[k]) W[n][k] and v_s[n] = sum_k shift_s[k] W[n][k], for the
+// 16 steps of a step group: a [16 steps x d] . [d x 64 columns] product per wave, on the matrix pipes. The fp32
+// (1 + scale) and shift rows enter as two 16-bit parts each (hi = the rounded value, lo = the rounded remainder:
+// ~2^-16 relative to the value with bf16, ~2^-22 with fp16) accumulated into the same fp32 sums; W in its own 16-bit
+// type. Wave = (step group, 64 output columns of W1 or Wqkv, layer): four 16x16 column tiles, u and v, so every W
+// element is read once per step group (230 MB at C2: the kernel's floor is that read). Operands straight from
+// global memory (a lane's 16 B of a W row and 32 B of each table row per 32 k), two K steps' loads in flight.
+// Earlier r06 forms: VALU FMAs on LDS-staged operands (~280 us per C2 call), then one operand part per wave (four
+// waves re-reading every W element: 160-180 us).
 template <typename T>
 __global__ __launch_bounds__(256) void lnfold_uv_kernel(LnFoldArgs a) {
-  __shared__ float Ws[64][65];
-  __shared__ float As[16][2][64];
-  const int t = threadIdx.x, n = t & 63, sq = t >> 6;
-  const int d = a.d, F = a.F, nbF = F / 64, nbQ = 3 * d / 64, nb = nbF + nbQ;
-  const int l = blockIdx.x / nb, j = blockIdx.x % nb;
+  typedef typename Op16<T>::v8 v8;
+  const int lane = threadIdx.x & 63;
+  const int d = a.d, F = a.F, nbF = F / 64, nb = nbF + 3 * d / 64, ng = (a.nfe + 15) / 16;
+  const int wv = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (wv >= a.depth * nb * ng) return;  // whole wave
+  const int g = wv % ng, j = (wv / ng) % nb, l = wv / (ng * nb);
   const bool ff = j < nbF;
   const int n0 = (ff ? j : j - nbF) * 64;
-  const T* W = reinterpret_cast<const T*>(ff ? a.w1[l] : a.wqkv[l]);
+  const T* wr = reinterpret_cast<const T*>(ff ? a.w1[l] : a.wqkv[l]) + (int64_t)(n0 + (lane & 15)) * d + 8 * (lane >> 4);
   // AdaLN row layout per layer (modules.py:321-323): shift_msa, scale_msa, gate_msa, shift_mlp, scale_mlp, gate_mlp
   const int64_t sh_off = (int64_t)l * 6 * d + (ff ? 3 : 0) * d, sc_off = sh_off + d;
-  const int64_t LW = 2 * (int64_t)F + 6 * (int64_t)d;
-  const int64_t u_off = a.out_off + l * LW + (ff ? 0 : 2 * (int64_t)F), v_off = u_off + (ff ? F : 3 * d);
-  for (int s0 = 0; s0 < a.nfe; s0 += 16) {
-    float au[4] = {0.f, 0.f, 0.f, 0.f}, av[4] = {0.f, 0.f, 0.f, 0.f};
-    for (int k0 = 0; k0 < d; k0 += 64) {
-      __syncthreads();
-      {  // W rows n0 .. n0+63, columns k0 .. k0+63: thread t takes row t >> 2, 16 columns
-        const int r = t >> 2, kq = (t & 3) * 16;
-        const T* src = W + (int64_t)(n0 + r) * d + k0 + kq;
+  const float* ar = a.table + (int64_t)min(g * 16 + (lane & 15), a.nfe - 1) * a.stride + 8 * (lane >> 4);
+  f32x4 acc[2][4] = {};
+  auto parts = [](const float4& p0, const float4& p1, float one, v8& hi, v8& lo) {
+    const float xv[8] = {p0.x, p0.y, p0.z, p0.w, p1.x, p1.y, p1.z, p1.w};
 #pragma unroll
-        for (int e = 0; e < 16; ++e) Ws[kq + e][r] = to_f32(src[e]);
-      }
-      {  // scale / shift of steps s0 .. s0+15 over the chunk: thread t takes step t >> 4, one of the two, 8 values
-        const int sl = t >> 4, which = (t >> 3) & 1, kq = (t & 7) * 8, s = s0 + sl;
-        const float* src = a.table + (int64_t)min(s, a.nfe - 1) * a.stride + (which ? sh_off : sc_off) + k0 + kq;
+    for (int e = 0; e < 8; ++e) {
+      const float x = one + xv[e];
+      hi[e] = from_f32<T>(x);
+      lo[e] = from_f32<T>(x - to_f32(hi[e]));
+    }
+  };
+  for (int k0 = 0; k0 < d; k0 += 64) {  // d % 64 == 0
+    float4 xs[2][2], xh[2][2];
+    v8 b[2][4];
 #pragma unroll
-        for (int e = 0; e < 8; ++e) As[sl][which][kq + e] = src[e];
-      }
-      __syncthreads();
-#pragma unroll 8
-      for (int k = 0; k < 64; ++k) {
-        const float w = Ws[k][n];
+    for (int u = 0; u < 2; ++u) {
+      const int k = k0 + 32 * u;
+      xs[u][0] = *reinterpret_cast<const float4*>(ar + sc_off + k);
+      xs[u][1] = *reinterpret_cast<const float4*>(ar + sc_off + k + 4);
+      xh[u][0] = *reinterpret_cast<const float4*>(ar + sh_off + k);
+      xh[u][1] = *reinterpret_cast<const float4*>(ar + sh_off + k + 4);
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          au[q] += (1.f + As[sq * 4 + q][0][k]) * w;
-          av[q] += As[sq * 4 + q][1][k] * w;
-        }
-      }
+      for (int t = 0; t < 4; ++t) b[u][t] = *reinterpret_cast<const v8*>(wr + (int64_t)t * 16 * d + k);
     }
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int s = s0 + sq * 4 + q;
-      if (s < a.nfe) {
-        a.table[(int64_t)s * a.stride + u_off + n0 + n] = au[q];
-        a.table[(int64_t)s * a.stride + v_off + n0 + n] = av[q];
+    for (int u = 0; u < 2; ++u) {
+      v8 shi, slo, hhi, hlo;
+      parts(xs[u][0], xs[u][1], 1.f, shi, slo);
+      parts(xh[u][0], xh[u][1], 0.f, hhi, hlo);
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        acc[0][t] = Op16<T>::mma16(shi, b[u][t], acc[0][t]);
+        acc[1][t] = Op16<T>::mma16(hhi, b[u][t], acc[1][t]);
+        acc[0][t] = Op16<T>::mma16(slo, b[u][t], acc[0][t]);
+        acc[1][t] = Op16<T>::mma16(hlo, b[u][t], acc[1][t]);
       }
     }
   }
+  // acc[uv][t][r]: step g*16 + 4 (lane >> 4) + r, column n0 + 16 t + (lane & 15)
+  const int64_t LW = 2 * (int64_t)F + 6 * (int64_t)d;
+  const int64_t u_off = a.out_off + l * LW + (ff ? 0 : 2 * (int64_t)F), v_off = u_off + (ff ? F : 3 * d);
+#pragma unroll
+  for (int t = 0; t < 4; ++t)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int s = g * 16 + 4 * (lane >> 4) + r;
+      if (s < a.nfe) {
+        float* o = a.table + (int64_t)s * a.stride + n0 + 16 * t + (lane & 15);
+        o[u_off] = acc[0][t][r];
+        o[v_off] = acc[1][t][r];
+      }
+    }
 }
 hipError_t lnfold_uv(int compute, const LnFoldArgs& a, hipStream_t st) {
   if (a.d % 64 || a.F % 64 || a.nfe <= 0 || a.depth <= 0) return hipErrorInvalidValue;
-  const dim3 grid(a.depth * (a.F / 64 + 3 * a.d / 64)), block(256);
+  const dim3 grid((a.depth * (a.F / 64 + 3 * a.d / 64) * ((a.nfe + 15) / 16) + 3) / 4), block(256);
   if (compute == F5H_C_BF16)
     hipLaunchKernelGGL(lnfold_uv_kernel<bf16>, grid, block, 0, st, a);
   else if (compute == F5H_C_FP16)

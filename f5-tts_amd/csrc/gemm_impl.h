@@ -319,17 +319,6 @@ F5H_DEV float sum8(float v) {
   v += dpp8<0x4E>(v);
   return v + dpp8<0x141>(v);
 }
-// Chan's pairwise combination of (count, mean, M2) partial statistics: (n, m, q) <- (n, m, q) + (nb, mb, qb)
-F5H_DEV void chan_add(float& n, float& m, float& q, float nb, float mb, float qb) {
-  const float nt = n + nb, f = nt > 0.f ? nb / nt : 0.f, dl = mb - m;
-  q = q + qb + dl * dl * n * f;
-  m = m + dl * f;
-  n = nt;
-}
-template <int CTRL>
-F5H_DEV void chan_dpp(float& n, float& m, float& q) {
-  chan_add(n, m, q, dpp8<CTRL>(n), dpp8<CTRL>(m), dpp8<CTRL>(q));
-}
 
 // Fast epilogue of one wave's sub-tile (whole-column tiles of the hot epilogues), per 16-row strip:
 // accumulators -> the wave's LDS strip (fp32, EPAD-float rows; one ds_write_b128 per block, the swapped-operand
@@ -380,10 +369,15 @@ F5H_DEV void epilogue_fast_t(const GemmArgs& g, const f32x4 (&acc)[MT][NT], floa
   } else if constexpr (LNF == 2) {
     lnA = load8(g.ln_u + col);
     lnB = load8(g.ln_v + col);
+    if constexpr (BIAS) {  // the bias joins v: one fused multiply-add pair per element below
+#pragma unroll
+      for (int e = 0; e < 8; ++e) lnB.v[e] += bias8.v[e];
+    }
     ln_st = rsrc_of(g.ln_part_in, (uint64_t)g.M * ln_np * 8);
   }
   const int lp0 = min(cc, ln_np - 1), lp1 = min(cc + 8, ln_np - 1);  // this lane's two partials (consumer)
-  const float ln_n0 = cc < ln_np ? 64.f : 0.f, ln_n1 = cc + 8 < ln_np ? 64.f : 0.f;
+  const float ln_w0 = cc < ln_np ? 1.f : 0.f, ln_w1 = cc + 8 < ln_np ? 1.f : 0.f;
+  const float ln_inv_np = 1.f / (float)ln_np, ln_inv_n = ln_inv_np * (1.f / 64.f);
   V8 gate8 = V8{{1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f}};
   if constexpr (EPI == EPI_RESID || EPI == EPI_RESID16)
     if (g.gate) gate8 = load8(g.gate + col);
@@ -503,17 +497,25 @@ F5H_DEV void epilogue_fast_t(const GemmArgs& g, const f32x4 (&acc)[MT][NT], floa
       V8 x{{a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w}};
       const RowIn& ri = rbuf[i % RB][t];
       if constexpr (LNF == 2) {
-        // the row's statistics from its strips' partials: two per lane, then across the row's 8 lanes
-        float n = ln_n0, m = __uint_as_float(ri.s0.x), qq = __uint_as_float(ri.s0.y);
-        chan_add(n, m, qq, ln_n1, __uint_as_float(ri.s1.x), __uint_as_float(ri.s1.y));
-        chan_dpp<0xB1>(n, m, qq);
-        chan_dpp<0x4E>(n, m, qq);
-        chan_dpp<0x141>(n, m, qq);
-        const float rstd = rsqrtf(qq / n + 1e-6f);  // LayerNorm eps 1e-6 (modules.py:316,336)
+        // the row's statistics from its strips' partials (two per lane, w0 / w1 = 1 where the partial exists):
+        // every strip holds 64 columns, so mean = the mean of the strip means and M2 = sum of the strips' M2 +
+        // 64 sum of (strip mean - mean)^2 (two sums over the row's 8 lanes, no division)
+        const float m0 = __uint_as_float(ri.s0.x), m1 = __uint_as_float(ri.s1.x);
+        const float m = sum8(ln_w0 * m0 + ln_w1 * m1) * ln_inv_np;
+        const float d0 = m0 - m, d1 = m1 - m;
+        const float qq = sum8(ln_w0 * (__uint_as_float(ri.s0.y) + 64.f * d0 * d0) +
+                              ln_w1 * (__uint_as_float(ri.s1.y) + 64.f * d1 * d1));
+        const float rstd = rsqrtf(qq * ln_inv_n + 1e-6f);  // LayerNorm eps 1e-6 (modules.py:316,336)
+        // x = rstd (x - m u) + (v + bias), as packed fp32 FMAs on column pairs
 #pragma unroll
-        for (int e = 0; e < 8; ++e) x.v[e] = rstd * (x.v[e] - m * lnA.v[e]) + lnB.v[e];
+        for (int e = 0; e < 8; e += 2) {
+          const f32x2 t = f32x2{x.v[e], x.v[e + 1]} - f32x2{m, m} * f32x2{lnA.v[e], lnA.v[e + 1]};
+          const f32x2 y = f32x2{rstd, rstd} * t + f32x2{lnB.v[e], lnB.v[e + 1]};
+          x.v[e] = y.x;
+          x.v[e + 1] = y.y;
+        }
       }
-      if constexpr (BIAS) {
+      if constexpr (BIAS && LNF != 2) {
 #pragma unroll
         for (int e = 0; e < 8; ++e) x.v[e] = add_nc(x.v[e], bias8.v[e]);
       }
@@ -553,19 +555,26 @@ F5H_DEV void epilogue_fast_t(const GemmArgs& g, const f32x4 (&acc)[MT][NT], floa
           // the stored (rounded) h values: hs = h (1 + scale) for the consumer, and this 64-column strip's
           // (mean, M2) of h (two passes over the row's 8 lanes)
           V8 hr, hv;
-          float sm = 0.f;
+          f32x2 s2 = {0.f, 0.f};
 #pragma unroll
-          for (int e = 0; e < 8; ++e) {
-            hr.v[e] = to_f32(from_f32<TC>(o.v[e]));
-            hv.v[e] = hr.v[e] * lnA.v[e];
-            sm += hr.v[e];
+          for (int e = 0; e < 8; e += 2) {
+            const f32x2 h2 = {to_f32(from_f32<TC>(o.v[e])), to_f32(from_f32<TC>(o.v[e + 1]))};
+            const f32x2 v2 = h2 * f32x2{lnA.v[e], lnA.v[e + 1]};
+            hr.v[e] = h2.x;
+            hr.v[e + 1] = h2.y;
+            hv.v[e] = v2.x;
+            hv.v[e + 1] = v2.y;
+            s2 += h2;
           }
           store8_rs<TC, AUX>(ln_dst, (uint32_t)((int64_t)row * g.ldc + col), hv);
-          const float mean = sum8(sm) * (1.f / 64.f);
-          float m2 = 0.f;
+          const float mean = sum8(s2.x + s2.y) * (1.f / 64.f);
+          f32x2 q2 = {0.f, 0.f};
 #pragma unroll
-          for (int e = 0; e < 8; ++e) m2 += (hr.v[e] - mean) * (hr.v[e] - mean);
-          m2 = sum8(m2);
+          for (int e = 0; e < 8; e += 2) {
+            const f32x2 dv = f32x2{hr.v[e], hr.v[e + 1]} - f32x2{mean, mean};
+            q2 += dv * dv;
+          }
+          const float m2 = sum8(q2.x + q2.y);
           // the row's 8 lanes store the same 8 bytes (no branch); rows >= M fall outside the descriptor
           __builtin_amdgcn_raw_buffer_store_b64(u32x2_t{__float_as_uint(mean), __float_as_uint(m2)}, ln_st,
                                                 (uint32_t)((row * ln_np + ln_p) * 8), 0, AUX);
