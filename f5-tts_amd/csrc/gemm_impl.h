@@ -336,18 +336,21 @@ F5H_DEV float sum8(float v) {
 // Shared by gemm_kernel and gemm_pp_kernel.
 // PD: strips of row data fetched ahead (1: the next strip's; fetching every strip's residual up front in the 256x256
 // ping-pong kernel measured equal at C4/C5, profiles/r05_ab_c4_c5_resid_prefetch.txt)
-// LNF (LayerNorm fold): 0 none, 1 producer (EPI_RESID16: also hs and the row-strip statistics), 2 consumer
-// (EPI_GELU_TANH / EPI_QKV: the normalisation applied to the accumulators); see GemmArgs.
+// LNF (LayerNorm fold): 0 none, 1 producer (EPI_RESID16: also hs and the row-strip statistics), 2 / 3 consumer
+// (EPI_GELU_TANH / EPI_QKV: the normalisation applied to the accumulators; 2 combines each row's strip partials
+// here, 3 reads the row's (mean, rstd) from ln_rows, which gemm_body filled from partials fetched before its K
+// loop); see GemmArgs.
 template <typename TC, int EPI, int MT, int NT, int WN, int EPAD, bool PREF, bool BIAS, int PM, int PT, int AUX = 0,
           int PD = 1, int LNF = 0>
 F5H_DEV void epilogue_fast_t(const GemmArgs& g, const f32x4 (&acc)[MT][NT], float* Cs, int rbase, int cbase,
-                             int lane, const V8 (&pre)[PM][PT]) {
+                             int lane, const V8 (&pre)[PM][PT], const float* ln_rows = nullptr) {
+  constexpr bool LNCONS = LNF == 2 || LNF == 3;
   constexpr int CH = WN / 8;          // 8-column chunks per strip row
   constexpr int TPC = 16 * CH / 64;   // chunks per lane per strip
   static_assert(64 % CH == 0 && (16 * CH) % 64 == 0, "whole chunks per lane");
   static_assert(LNF == 0 || (WN == 64 && is16<TC>()), "the LayerNorm fold: 64-column wave strips, 16-bit operands");
   static_assert(LNF != 1 || EPI == EPI_RESID16, "fold producer: the 16-bit residual epilogue");
-  static_assert(LNF != 2 || EPI == EPI_GELU_TANH || EPI == EPI_QKV, "fold consumer: FFN1 or QKV");
+  static_assert(!LNCONS || EPI == EPI_GELU_TANH || EPI == EPI_QKV, "fold consumer: FFN1 or QKV");
   const int fr = lane & 15, q = lane >> 4;
   const int cc = lane % CH;
   const int col = cbase + cc * 8;
@@ -366,14 +369,14 @@ F5H_DEV void epilogue_fast_t(const GemmArgs& g, const f32x4 (&acc)[MT][NT], floa
     ln_dst = rsrc_of(g.hs, (uint64_t)g.M * g.ldc * sizeof(TC));
     ln_st = rsrc_of(g.ln_part, (uint64_t)g.M * ln_np * 8);
     ln_p = __builtin_amdgcn_readfirstlane(cbase >> 6);
-  } else if constexpr (LNF == 2) {
+  } else if constexpr (LNCONS) {
     lnA = load8(g.ln_u + col);
     lnB = load8(g.ln_v + col);
     if constexpr (BIAS) {  // the bias joins v: one fused multiply-add pair per element below
 #pragma unroll
       for (int e = 0; e < 8; ++e) lnB.v[e] += bias8.v[e];
     }
-    ln_st = rsrc_of(g.ln_part_in, (uint64_t)g.M * ln_np * 8);
+    if constexpr (LNF == 2) ln_st = rsrc_of(g.ln_part_in, (uint64_t)g.M * ln_np * 8);
   }
   const int lp0 = min(cc, ln_np - 1), lp1 = min(cc + 8, ln_np - 1);  // this lane's two partials (consumer)
   const float ln_w0 = cc < ln_np ? 1.f : 0.f, ln_w1 = cc + 8 < ln_np ? 1.f : 0.f;
@@ -496,16 +499,23 @@ F5H_DEV void epilogue_fast_t(const GemmArgs& g, const f32x4 (&acc)[MT][NT], floa
       const float4 a0 = *reinterpret_cast<const float4*>(src), a1 = *reinterpret_cast<const float4*>(src + 4);
       V8 x{{a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w}};
       const RowIn& ri = rbuf[i % RB][t];
-      if constexpr (LNF == 2) {
+      if constexpr (LNCONS) {
+        float m, rstd;
+        if constexpr (LNF == 3) {
+          const float2 ms = *reinterpret_cast<const float2*>(ln_rows + 2 * (i * 16 + rr));
+          m = ms.x;
+          rstd = ms.y;
+        } else {
         // the row's statistics from its strips' partials (two per lane, w0 / w1 = 1 where the partial exists):
         // every strip holds 64 columns, so mean = the mean of the strip means and M2 = sum of the strips' M2 +
         // 64 sum of (strip mean - mean)^2 (two sums over the row's 8 lanes, no division)
         const float m0 = __uint_as_float(ri.s0.x), m1 = __uint_as_float(ri.s1.x);
-        const float m = sum8(ln_w0 * m0 + ln_w1 * m1) * ln_inv_np;
+        m = sum8(ln_w0 * m0 + ln_w1 * m1) * ln_inv_np;
         const float d0 = m0 - m, d1 = m1 - m;
         const float qq = sum8(ln_w0 * (__uint_as_float(ri.s0.y) + 64.f * d0 * d0) +
                               ln_w1 * (__uint_as_float(ri.s1.y) + 64.f * d1 * d1));
-        const float rstd = rsqrtf(qq * ln_inv_n + 1e-6f);  // LayerNorm eps 1e-6 (modules.py:316,336)
+        rstd = rsqrtf(qq * ln_inv_n + 1e-6f);  // LayerNorm eps 1e-6 (modules.py:316,336)
+        }
         // x = rstd (x - m u) + (v + bias), as packed fp32 FMAs on column pairs
 #pragma unroll
         for (int e = 0; e < 8; e += 2) {
@@ -515,7 +525,7 @@ F5H_DEV void epilogue_fast_t(const GemmArgs& g, const f32x4 (&acc)[MT][NT], floa
           x.v[e + 1] = y.y;
         }
       }
-      if constexpr (BIAS && LNF != 2) {
+      if constexpr (BIAS && !LNCONS) {
 #pragma unroll
         for (int e = 0; e < 8; ++e) x.v[e] = add_nc(x.v[e], bias8.v[e]);
       }
@@ -621,7 +631,7 @@ F5H_DEV void epilogue_fast_t(const GemmArgs& g, const f32x4 (&acc)[MT][NT], floa
 }
 template <typename TC, int EPI, int MT, int NT, int WN, int EPAD, bool PREF, int AUX = 0, int PD = 1, int PM, int PT>
 F5H_DEV void epilogue_fast(const GemmArgs& g, const f32x4 (&acc)[MT][NT], float* Cs, int rbase, int cbase,
-                           int lane, const V8 (&pre)[PM][PT]) {
+                           int lane, const V8 (&pre)[PM][PT], const float* ln_rows = nullptr) {
   // LayerNorm fold forms (GemmArgs hs / ln_part_in: 16-bit, 64-column wave strips; bias always present there)
   if constexpr (WN == 64 && is16<TC>() && AUX == 0) {
     if constexpr (EPI == EPI_RESID16) {
@@ -633,6 +643,15 @@ F5H_DEV void epilogue_fast(const GemmArgs& g, const f32x4 (&acc)[MT][NT], float*
         return;
       }
     } else if constexpr (EPI == EPI_GELU_TANH || EPI == EPI_QKV) {
+      if (g.ln_part_in && ln_rows) {
+        if (g.bias)
+          epilogue_fast_t<TC, EPI, MT, NT, WN, EPAD, PREF, true, PM, PT, AUX, PD, 3>(g, acc, Cs, rbase, cbase, lane, pre,
+                                                                                   ln_rows);
+        else
+          epilogue_fast_t<TC, EPI, MT, NT, WN, EPAD, PREF, false, PM, PT, AUX, PD, 3>(g, acc, Cs, rbase, cbase, lane, pre,
+                                                                                    ln_rows);
+        return;
+      }
       if (g.ln_part_in) {
         if (g.bias)
           epilogue_fast_t<TC, EPI, MT, NT, WN, EPAD, PREF, true, PM, PT, AUX, PD, 2>(g, acc, Cs, rbase, cbase, lane, pre);
@@ -1018,7 +1037,23 @@ F5H_DEV void gemm_body(const GemmArgs& g, const int b, const int nwg, uint4* lds
       }
   }
 
-  constexpr int NPRE = PREF ? MT * TPS : 0;  // residual loads issued behind the first stages
+  // LayerNorm fold consumer (QKV / FFN1 with GemmArgs ln_part_in): thread t < BM fetches the strip partials of the
+  // block's row t (16 x 8 B) behind the first stages, and combines them after the K loop into the row's (mean,
+  // rstd) in LDS, once per row (the strip epilogue's LNF 2 form combines them per chunk row, 8 lanes per row and
+  // again in every column tile's waves). Issued whether or not the fold is on (a null descriptor reads zeros with
+  // no memory access), so the first stage wait's count is a constant.
+  constexpr bool LNC = (EPI == EPI_QKV || EPI == EPI_GELU_TANH) && is16<TC>() && WN == 64 && FAST && NT % 2 == 0 &&
+                       !CHAIN && !PUB && BM <= C::THREADS;
+  u32x4 lnraw[LNC ? 8 : 1];
+  if constexpr (LNC) {
+    const bool on = g.ln_part_in != nullptr;
+    const __amdgpu_buffer_rsrc_t st = rsrc_of(g.ln_part_in, on ? (uint64_t)g.M * g.ln_nparts * 8 : 0);
+    const uint32_t base = tid < BM ? (uint32_t)(min(m0 + tid, g.M - 1) * g.ln_nparts * 8) : 0xFFFFFF00u;
+#pragma unroll
+    for (int e = 0; e < 8; ++e)
+      lnraw[e] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(st, base + 16 * e, 0, 0));
+  }
+  constexpr int NPRE = PREF ? MT * TPS : (LNC ? 8 : 0);  // loads issued behind the first stages
   for (int kt = 0; kt < nk; ++kt) {
     // stage kt has landed for THIS wave once at most the younger in-flight stages remain;
     // the barrier then publishes every wave's part of it
@@ -1095,6 +1130,32 @@ F5H_DEV void gemm_body(const GemmArgs& g, const int b, const int nwg, uint4* lds
   __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0), expcnt/lgkmcnt untouched
   __syncthreads();
   probe_mark(g.probe, probe_t, 2);
+  // the fold consumer's row statistics, past the wave strips: (mean, rstd) of block row r at [2r, 2r + 2)
+  float* const ln_rows = reinterpret_cast<float*>(lds) + NW * 16 * C::EPAD;
+  if constexpr (LNC) {
+    static_assert(C::bytes >= (NW * 16 * C::EPAD + 2 * BM) * 4, "LDS for the fold's row statistics");
+    if (g.ln_part_in) {  // uniform
+      if (tid < BM) {
+        // every strip holds 64 columns: mean = the mean of the strip means, M2 = sum of the strips' M2 + 64 sum of
+        // (strip mean - mean)^2 (partials past ln_nparts weigh 0)
+        const int np = g.ln_nparts;
+        const float inv_np = 1.f / (float)np;
+        float sm = 0.f;
+#pragma unroll
+        for (int p = 0; p < 16; ++p) sm += p < np ? __uint_as_float(lnraw[p >> 1][(p & 1) * 2]) : 0.f;
+        const float mean = sm * inv_np;
+        float q = 0.f;
+#pragma unroll
+        for (int p = 0; p < 16; ++p) {
+          const float dm = __uint_as_float(lnraw[p >> 1][(p & 1) * 2]) - mean;
+          q += p < np ? __uint_as_float(lnraw[p >> 1][(p & 1) * 2 + 1]) + 64.f * dm * dm : 0.f;
+        }
+        ln_rows[2 * tid] = mean;
+        ln_rows[2 * tid + 1] = rsqrtf(q * inv_np * (1.f / 64.f) + 1e-6f);  // LayerNorm eps 1e-6 (modules.py:316,336)
+      }
+      __syncthreads();
+    }
+  }
 
   // ---- epilogue, per wave and 16-row strip: accumulators -> the wave's LDS strip (fp32,
   // padded rows) -> 8-column chunks of whole rows, so the epilogue's global accesses are
@@ -1111,7 +1172,7 @@ F5H_DEV void gemm_body(const GemmArgs& g, const int b, const int nwg, uint4* lds
   static_assert(FAST_EPI || !PUB, "the chain publishes after the fast (LDS-strip) epilogue");
   if constexpr (FAST_EPI) {
     epilogue_fast<TC, EPI, MT, NT, WN, C::EPAD, PREF, PUB ? kAuxWT : 0>(g, acc, Cs, m0 + wm * WM, n0 + wn * WN, lane,
-                                                                         pre);
+                                                                         pre, LNC ? ln_rows + 2 * wm * WM : nullptr);
     if constexpr (PUB) chain_publish(dep, g.M, m0, BM);
   }
   if constexpr (!FAST_EPI) {

@@ -8,6 +8,8 @@ Tolerances (written here):
     own bf16 / fp16 error vs its fp32 output on the same inputs.
 """
 
+import contextlib
+import os
 import threading
 
 import numpy as np
@@ -377,10 +379,10 @@ def test_graph_eviction_never_waits_for_other_streams():
     entry) return to the host long before it ends (the old eviction synchronised the device).
 
     Round 5 saw one failure of this test inside the full suite (the first evicting call took 0.83 s; alone it
-    passed). The timed region is now the sample call on device-resident inputs (the pageable host->device copies
-    of the old form go through HIP's staging path, whose placement on hardware queues the process's earlier
-    streams decide), and every call records the engine's host time by phase (f5h_last_call_host_ms), the torch
-    caching allocator's device allocations / frees / allocation retries / all-stream synchronisations and the
+    passed). Cause (round 6): hardware-queue sharing between the spin's stream and the engine's, which depends on
+    how many streams the process created before (see the spin below). The timed region is the sample call on
+    device-resident inputs, and every call records the engine's host time by phase (f5h_last_call_host_ms), the
+    torch caching allocator's device allocations / frees / allocation retries / all-stream synchronisations and the
     reserved memory, so a slow call names its phase in the failure message."""
     _need_gpu()
     import time
@@ -399,7 +401,13 @@ def test_graph_eviction_never_waits_for_other_streams():
         return [st.get(k, 0) for k in ("num_device_alloc", "num_device_free", "num_alloc_retries",
                                        "num_sync_all_streams")] + [torch.cuda.memory_reserved()]
 
-    other = torch.cuda.Stream()
+    # The spin runs on a high-priority stream: HIP multiplexes same-priority streams onto GPU_MAX_HW_QUEUES (4)
+    # hardware queues that run their packets in order, so a default-priority spin stream can share the hardware
+    # queue of the stream the engine runs on and hold its kernels back for the rest of the spin, whatever the
+    # engine does (round 5's 0.83 s failure; tools/diag_hwqueue.py, profiles/r06_diag_hwqueue.txt: a default-stream
+    # kernel waited 418 ms behind a spin on an unrelated stream for one of eight stream-creation counts). Streams of
+    # another priority get hardware queues of their own.
+    other = torch.cuda.Stream(priority=-1)
     with torch.cuda.stream(other):
         torch.cuda._sleep(int(2.0e9))  # ~1 s of spinning on another stream
     took, rows = [], []
@@ -599,6 +607,16 @@ def test_cfg_branch_chains_bitwise_equal(compute):
         assert torch.equal(outs[mode][1], outs["one"][1]), mode
 
 
+@contextlib.contextmanager
+def _fold_off(eng):
+    """The phase chain runs the LayerNorm launches (the fold is off on a chained call: engine.cpp c.lnfold), so the
+    chain tests compare against unchained calls with the fold off too (bitwise)."""
+    eng.set_ln_fold(False)
+    try:
+        yield
+    finally:
+        eng.set_ln_fold(os.environ.get("F5H_LNFOLD", "1") != "0")
+
 @pytest.mark.parametrize("compute", ["bf16", "fp16"])
 def test_phase_chain_bitwise_equal(compute):
     """The in-launch phase chain (f5h_set_chain: out-proj .. FFN2 + the next layer's LayerNorm and QKV as one
@@ -611,6 +629,8 @@ def test_phase_chain_bitwise_equal(compute):
     arch = configs.get_arch("F5TTS_v1_Base", depth=3)
     m = _model(arch, compute)
     eng = m.transformer.get_engine(compute, m.device)
+    fold = _fold_off(eng)
+    fold.__enter__()
     try:
         for ref, total, nt in ((37, 149, 20), (250, 611, 60)):
             inp = synthetic.make_case(B=1, ref_frames=[ref], total_frames=[total], n_text=[nt],
@@ -645,6 +665,7 @@ def test_phase_chain_bitwise_equal(compute):
         eng.set_chain(False)
         eng.set_graph_mode(True)
         eng.set_cfg_streams(0)
+        fold.__exit__(None, None, None)
 
 
 @pytest.mark.parametrize("compute", ["bf16", "fp16"])
@@ -663,16 +684,17 @@ def test_phase_chain_c2_graph_replays_bitwise_equal(compute):
     y0 = synthetic.reference_noise(dur, gc.SEED)
     kw = dict(cond=inp["cond"].to(DEV), text=inp["text"].to(DEV), duration=inp["duration"], lens=inp["lens"],
               steps=16, cfg_strength=2.0, sway_sampling_coef=-1.0, y0=y0.to(DEV), keep_trajectory=False)
-    try:
-        eng.set_chain(False)
-        plain = m.sample(**kw)[0].clone()
-        eng.set_chain(True)
-        n0 = eng.chain_stats()[0]
-        outs = [m.sample(**kw)[0].clone() for _ in range(4)]
-        torch.cuda.synchronize()
-        n1, fault, _ = eng.chain_stats()
-    finally:
-        eng.set_chain(False)
+    with _fold_off(eng):
+        try:
+            eng.set_chain(False)
+            plain = m.sample(**kw)[0].clone()
+            eng.set_chain(True)
+            n0 = eng.chain_stats()[0]
+            outs = [m.sample(**kw)[0].clone() for _ in range(4)]
+            torch.cuda.synchronize()
+            n1, fault, _ = eng.chain_stats()
+        finally:
+            eng.set_chain(False)
     assert n1 - n0 == arch["depth"], "one capture of the chained step graph, replayed by every call"
     assert fault == 0
     for i, o in enumerate(outs):
@@ -700,6 +722,8 @@ def test_phase_chain_give_up_fails_loudly():
     m = _model(arch, "bf16")
     eng = m.transformer.get_engine("bf16", m.device)
     kw = _chain_case(arch, 611, 5)
+    fold = _fold_off(eng)
+    fold.__enter__()
     eng.set_chain(False)
     plain, _ = m.sample(**kw)
     plain = plain.clone()
@@ -726,6 +750,7 @@ def test_phase_chain_give_up_fails_loudly():
         eng.set_chain(False)
     fixed, _ = m.sample(**kw)
     torch.cuda.synchronize()
+    fold.__exit__(None, None, None)
     assert torch.equal(fixed, plain) and eng.chain_stats()[1] == 0
 
 
@@ -743,6 +768,7 @@ def test_phase_chain_concurrent_streams():
     m = _model(arch, "bf16")
     eng = m.transformer.get_engine("bf16", m.device)
     eng.set_chain(True)  # (off by default)
+    eng.set_ln_fold(False)  # a refused chained call runs the separate launches: bitwise the chained result
     cases = [[_chain_case(arch, 1876, 10 + 2 * t + i) for i in range(3)] for t in range(2)]
     streams = [torch.cuda.Stream(), torch.cuda.Stream()]
 
@@ -778,6 +804,8 @@ def test_phase_chain_concurrent_streams():
             for a, b in zip(par[t], seq[t]):
                 assert torch.equal(a, b), t
     n, fault, r1 = eng.chain_stats()
+    eng.set_chain(False)
+    eng.set_ln_fold(os.environ.get("F5H_LNFOLD", "1") != "0")
     print(f"concurrent chains: sequential {t_seq * 1e3:.1f} ms, two threads {[round(w * 1e3, 1) for w in walls]} ms "
           f"for 2 x 3 calls; chained calls sent to the separate launches: {r1 - r0}; chain launches {n}")
     assert fault == 0
