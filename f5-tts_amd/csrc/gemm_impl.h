@@ -315,9 +315,23 @@ F5H_DEV float dpp8(float x) {
   return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), CTRL, 0xF, 0xF, false));
 }
 F5H_DEV float sum8(float v) {
-  v += dpp8<0xB1>(v);
-  v += dpp8<0x4E>(v);
-  return v + dpp8<0x141>(v);
+  v = add_nc(v, dpp8<0xB1>(v));
+  v = add_nc(v, dpp8<0x4E>(v));
+  return add_nc(v, dpp8<0x141>(v));
+}
+// The LayerNorm fold's row statistics from 64-column strip partials (mean m_p, M2 q_p): mean = the mean of the strip
+// means, M2 = sum_p (q_p + 64 (m_p - mean)^2); a strip's term and the final rstd (LayerNorm eps 1e-6,
+// modules.py:316,336), each rounding explicit so the per-chunk-row form (LNF 2) and the once-per-row form
+// (ln_row_stats, LNF 3) agree bit for bit
+F5H_DEV float ln_m2_term(float q, float mp, float mean) {
+  const float d = sub_nc(mp, mean);
+  return __builtin_fmaf(mul_nc(64.f, d), d, q);
+}
+F5H_DEV float ln_rstd(float m2, float inv_np) { return rsqrtf(__builtin_fmaf(m2, mul_nc(inv_np, 1.f / 64.f), 1e-6f)); }
+// the 8-lane DPP sum of sum8 over lanes c = 0..7 holding a_c: ((a0 + a1) + (a2 + a3)) + ((a4 + a5) + (a6 + a7)) in
+// every lane (xor 1, xor 2, then the half mirror: lane c adds lane 7 - c, whose pairs are the same sums)
+F5H_DEV float sum8_order(const float (&a)[8]) {
+  return add_nc(add_nc(add_nc(a[0], a[1]), add_nc(a[2], a[3])), add_nc(add_nc(a[4], a[5]), add_nc(a[6], a[7])));
 }
 
 // Fast epilogue of one wave's sub-tile (whole-column tiles of the hot epilogues), per 16-row strip:
@@ -380,7 +394,7 @@ F5H_DEV void epilogue_fast_t(const GemmArgs& g, const f32x4 (&acc)[MT][NT], floa
   }
   const int lp0 = min(cc, ln_np - 1), lp1 = min(cc + 8, ln_np - 1);  // this lane's two partials (consumer)
   const float ln_w0 = cc < ln_np ? 1.f : 0.f, ln_w1 = cc + 8 < ln_np ? 1.f : 0.f;
-  const float ln_inv_np = 1.f / (float)ln_np, ln_inv_n = ln_inv_np * (1.f / 64.f);
+  const float ln_inv_np = 1.f / (float)ln_np;
   V8 gate8 = V8{{1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f}};
   if constexpr (EPI == EPI_RESID || EPI == EPI_RESID16)
     if (g.gate) gate8 = load8(g.gate + col);
@@ -509,12 +523,11 @@ F5H_DEV void epilogue_fast_t(const GemmArgs& g, const f32x4 (&acc)[MT][NT], floa
         // the row's statistics from its strips' partials (two per lane, w0 / w1 = 1 where the partial exists):
         // every strip holds 64 columns, so mean = the mean of the strip means and M2 = sum of the strips' M2 +
         // 64 sum of (strip mean - mean)^2 (two sums over the row's 8 lanes, no division)
+        // (every rounding written out: ln_row_stats below gives the same bits from one thread)
         const float m0 = __uint_as_float(ri.s0.x), m1 = __uint_as_float(ri.s1.x);
-        m = sum8(ln_w0 * m0 + ln_w1 * m1) * ln_inv_np;
-        const float d0 = m0 - m, d1 = m1 - m;
-        const float qq = sum8(ln_w0 * (__uint_as_float(ri.s0.y) + 64.f * d0 * d0) +
-                              ln_w1 * (__uint_as_float(ri.s1.y) + 64.f * d1 * d1));
-        rstd = rsqrtf(qq * ln_inv_n + 1e-6f);  // LayerNorm eps 1e-6 (modules.py:316,336)
+        m = mul_nc(sum8(add_nc(ln_w0 * m0, ln_w1 * m1)), ln_inv_np);
+        const float e0 = ln_m2_term(__uint_as_float(ri.s0.y), m0, m), e1 = ln_m2_term(__uint_as_float(ri.s1.y), m1, m);
+        rstd = ln_rstd(sum8(add_nc(ln_w0 * e0, ln_w1 * e1)), ln_inv_np);
         }
         // x = rstd (x - m u) + (v + bias), as packed fp32 FMAs on column pairs
 #pragma unroll
@@ -1138,20 +1151,25 @@ F5H_DEV void gemm_body(const GemmArgs& g, const int b, const int nwg, uint4* lds
       if (tid < BM) {
         // every strip holds 64 columns: mean = the mean of the strip means, M2 = sum of the strips' M2 + 64 sum of
         // (strip mean - mean)^2 (partials past ln_nparts weigh 0)
+        // the epilogue's per-chunk-row form, bit for bit: lane c of the row's 8 held partials c and c + 8
         const int np = g.ln_nparts;
         const float inv_np = 1.f / (float)np;
-        float sm = 0.f;
+        auto mp = [&](int p) { return __uint_as_float(lnraw[p >> 1][(p & 1) * 2]); };
+        auto qp = [&](int p) { return __uint_as_float(lnraw[p >> 1][(p & 1) * 2 + 1]); };
+        float a[8], e[8];
 #pragma unroll
-        for (int p = 0; p < 16; ++p) sm += p < np ? __uint_as_float(lnraw[p >> 1][(p & 1) * 2]) : 0.f;
-        const float mean = sm * inv_np;
-        float q = 0.f;
+        for (int c = 0; c < 8; ++c) {
+          const float w0 = c < np ? 1.f : 0.f, w1 = c + 8 < np ? 1.f : 0.f;
+          a[c] = add_nc(w0 * mp(c), w1 * mp(c + 8));
+        }
+        const float mean = mul_nc(sum8_order(a), inv_np);
 #pragma unroll
-        for (int p = 0; p < 16; ++p) {
-          const float dm = __uint_as_float(lnraw[p >> 1][(p & 1) * 2]) - mean;
-          q += p < np ? __uint_as_float(lnraw[p >> 1][(p & 1) * 2 + 1]) + 64.f * dm * dm : 0.f;
+        for (int c = 0; c < 8; ++c) {
+          const float w0 = c < np ? 1.f : 0.f, w1 = c + 8 < np ? 1.f : 0.f;
+          e[c] = add_nc(w0 * ln_m2_term(qp(c), mp(c), mean), w1 * ln_m2_term(qp(c + 8), mp(c + 8), mean));
         }
         ln_rows[2 * tid] = mean;
-        ln_rows[2 * tid + 1] = rsqrtf(q * inv_np * (1.f / 64.f) + 1e-6f);  // LayerNorm eps 1e-6 (modules.py:316,336)
+        ln_rows[2 * tid + 1] = ln_rstd(sum8_order(e), inv_np);
       }
       __syncthreads();
     }
@@ -1959,8 +1977,11 @@ static hipError_t launch_t(const GemmArgs& a, hipStream_t st) {
   if (a.M == 0) return hipSuccess;
   int cfg = 0;
   if constexpr (is16<TC>()) cfg = gemm_select_cfg(a);
-  // the LayerNorm fold runs only in the strip epilogue of the 64-column-strip configurations (0, 1, 5, 11): refuse
-  // it anywhere else rather than ignore it (the results would be those of an unnormalised operand)
+  // the LayerNorm fold runs only in the strip epilogue of the 64-column-strip configurations (0, 1, 5, 11): a forced
+  // 256x256 configuration without it (12: 32-column quadrant strips, 13: register-only epilogue) runs as cfg 11, the
+  // same tile (every configuration gives the same bits); anything else is refused rather than ignored (the results
+  // would be those of an unnormalised operand)
+  if ((a.hs || a.ln_part_in) && (cfg == 12 || cfg == 13)) cfg = 11;
   if (a.hs || a.ln_part_in) {
     const bool prod = a.hs && EPI == EPI_RESID16 && a.hs_scale && a.ln_part;
     const bool cons = a.ln_part_in && (EPI == EPI_GELU_TANH || EPI == EPI_QKV) && a.ln_u && a.ln_v;

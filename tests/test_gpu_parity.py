@@ -128,6 +128,49 @@ def test_sample_bitwise_identical_across_tile_configs(compute):
         assert torch.equal(o, outs[0]), cfg
 
 
+@pytest.mark.parametrize("compute", ["bf16", "fp16"])
+@pytest.mark.parametrize("preset,depth", [("F5TTS_v1_Base", 2), ("F5TTS_v1_Small_4L", 2)])
+def test_ln_fold_bitwise_identical_across_tile_configs(compute, preset, depth):
+    """The LayerNorm fold (single-utterance DiT calls; DESIGN.md §3 'LayerNorm fold') under every tile configuration:
+    bitwise identical. The consumers combine the producers' 64-column strip statistics either once per block row
+    (gemm_kernel configurations 0/1/5) or per chunk row in the strip epilogue (the 256x256 kernels; 12 and 13 run
+    the fold as 11), with every rounding written out so both forms give the same bits; d = 1024 (16 strips) and
+    d = 768 (12: lanes holding one partial or none). Against the unfolded launches the result moves by the
+    statistics' summation order only (rel-L2 well under the bf16 / fp16 rounding of the output)."""
+    _need_gpu()
+    from f5_tts_amd import configs
+
+    arch = configs.get_arch(preset, depth=depth)
+    m = _model(arch, compute)
+    eng = m.transformer.get_engine(compute, m.device)
+    inp = synthetic.make_case(B=1, ref_frames=[300], total_frames=[777], n_text=[90])
+    dur = torch.tensor([777])
+    y0 = synthetic.reference_noise(dur, 7)
+    kw = dict(cond=inp["cond"].to(DEV), text=inp["text"].to(DEV), duration=dur.to(DEV), lens=inp["lens"].to(DEV),
+              y0=y0.to(DEV), steps=3, cfg_strength=2.0, sway_sampling_coef=-1.0, keep_trajectory=False)
+    outs = []
+    try:
+        eng.set_ln_fold(True)
+        sup, p0 = eng.ln_fold_stats()
+        assert sup, "the fold should be supported for this architecture"
+        for cfg in GEMM_CONFIGS:
+            gemm_force_config(cfg)
+            outs.append(m.sample(**kw)[0].clone())
+        _, p1 = eng.ln_fold_stats()
+        assert p1 > p0, "no backbone pass ran with the fold"
+        eng.set_ln_fold(False)
+        gemm_force_config(-1)
+        plain = m.sample(**kw)[0]
+    finally:
+        gemm_force_config(-1)
+        eng.set_ln_fold(os.environ.get("F5H_LNFOLD", "1") != "0")
+    assert torch.isfinite(outs[0]).all()
+    for cfg, o in zip(GEMM_CONFIGS, outs):
+        assert torch.equal(o, outs[0]), cfg
+    rel = float((outs[0].float() - plain.float()).norm() / plain.float().norm())
+    assert rel < (1e-2 if compute == "bf16" else 2e-3), rel
+
+
 @pytest.mark.parametrize("compute,tol", [("fp32", 1e-5), ("bf16", 2e-2), ("fp16", 4e-3)])
 @pytest.mark.parametrize("S,H,N,masked", [(2, 16, 1876, False), (3, 2, 150, True), (1, 1, 65, False),
                                           (2, 4, 577, True)])
