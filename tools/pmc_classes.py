@@ -23,6 +23,9 @@ import sys
 from collections import defaultdict
 
 ORDER = {-2: "norm1", -1: "qkv", 1: "out", 2: "norm", 3: "ffn1", 4: "ffn2"}
+# with the LayerNorm fold (round 6) the FFN-norm launch is gone and layers after the first have no
+# attention-norm either: attention is followed by out, FFN1, FFN2 directly
+ORDER_FOLD = {-2: "norm1", -1: "qkv", 1: "out", 2: "ffn1", 3: "ffn2"}
 GEMMS = ("qkv", "out", "ffn1", "ffn2")
 # launch shapes as bench.py names them (S = CFG-packed sequences, L = padded frames), FFN width
 SHAPES = {"c2": dict(config="c2", S=2, L=1876, dim=1024, depth=22, ff=2048),
@@ -60,7 +63,8 @@ def classify(disp):
     for i, (_, name, _) in enumerate(disp):
         if "attn16" in name or "attn_f32" in name:
             cls[i] = "attention"
-            for off, c in ORDER.items():
+            folded = i + 2 < len(disp) and "gemm" in disp[i + 2][1] and "chain_kernel" not in disp[i + 2][1]
+            for off, c in (ORDER_FOLD if folded else ORDER).items():
                 if 0 <= i + off < len(disp) and "chain_kernel" not in disp[i + off][1] and \
                         ("gemm" in disp[i + off][1]) == (c in GEMMS):
                     cls.setdefault(i + off, c)
