@@ -391,6 +391,31 @@ __global__ __launch_bounds__(256) void rms16_kernel(const T* h, int M, const flo
   }
 }
 
+template <typename T>
+__global__ __launch_bounds__(256) void scale_cols_kernel(const T* W, int64_t n8, int K, const float* g, T* out) {
+  typedef typename Op16<T>::v8 v8;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n8; i += (int64_t)gridDim.x * blockDim.x) {
+    const int k0 = (int)((i * 8) % K);
+    const v8 w = reinterpret_cast<const v8*>(W)[i];
+    v8 o;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) o[e] = from_f32<T>(to_f32(w[e]) * g[k0 + e]);
+    reinterpret_cast<v8*>(out)[i] = o;
+  }
+}
+hipError_t scale_cols(int compute, const void* W, int64_t rows, int K, const float* g, void* out, hipStream_t st) {
+  if (K % 8 || rows <= 0) return hipErrorInvalidValue;
+  const int64_t n8 = rows * K / 8;
+  const dim3 gr((unsigned)std::min<int64_t>((n8 + 255) / 256, 4096)), b(256);
+  if (compute == F5H_C_BF16)
+    hipLaunchKernelGGL(scale_cols_kernel<bf16>, gr, b, 0, st, (const bf16*)W, n8, K, g, (bf16*)out);
+  else if (compute == F5H_C_FP16)
+    hipLaunchKernelGGL(scale_cols_kernel<f16>, gr, b, 0, st, (const f16*)W, n8, K, g, (f16*)out);
+  else
+    return hipErrorInvalidValue;
+  return hipGetLastError();
+}
+
 hipError_t rms_norm_g(int compute, const void* hv, int h16, int M, int d, const float* g, void* out, hipStream_t st) {
   if (d % 4 || d > 4 * 64 * MAXV) return hipErrorInvalidValue;
   const dim3 gr(nblk(M, 4)), b(256);

@@ -65,6 +65,7 @@ struct CNX {
 struct Layer {
   Lin qkv, out, ff1, ff2, skip;  // skip: UNetT skip_proj [d][2d] over cat(x, skip) (later half)
   float *g_attn = nullptr, *g_ff = nullptr;  // UNetT RMSNorm gains
+  Lin qkv_g, ff1_g;  // UNetT RMSNorm fold: qkv / ff1 with the norm's gain folded in, W diag(g) (same bias)
 };
 
 struct GraphKey {
@@ -130,8 +131,10 @@ struct f5h_engine {
   // launches of their own. f5h_set_ln_fold, env F5H_LNFOLD=0 at creation turns it off. lnf_ok: the engine supports
   // it (DiT, 16-bit, dim and ff a multiple of 64, dim <= 1024); lnf_w: device array [W1 of every layer, Wqkv of every
   // layer] for lnfold_uv; ada_row: floats per AdaLN table row (the modulation rows, then per layer the fold's u/v).
+  // The same switch covers the UNetT RMSNorm fold (rmsf_ok: 16-bit UNetT, dim a multiple of 64, dim <= 1024; the
+  // consumers read the residual stream with W diag(g), Layer::qkv_g / ff1_g).
   int lnfold = 1;
-  bool lnf_ok = false;
+  bool lnf_ok = false, rmsf_ok = false;
   const void** lnf_w = nullptr;
   int64_t ada_row = 0;
   std::atomic<int64_t> n_lnfold{0};  // backbone passes enqueued with the fold
@@ -549,7 +552,7 @@ static void layout(const f5h_engine* e, WS& ws, Bufs& b, int B, int N, int nfe, 
   b.chain = a.backbone == F5H_DIT ? ws.take<unsigned>((size_t)a.depth * 5 * b.chain_g4) : nullptr;
   b.ada_cur = a.backbone == F5H_DIT ? ws.take<float>((size_t)e->ada_row) : nullptr;
   // LayerNorm fold: per row and 64-column strip of the residual stream, (mean, M2) (float2)
-  b.lnp = e->lnf_ok ? ws.take<float>(rows * (size_t)(d / 64) * 2) : nullptr;
+  b.lnp = (e->lnf_ok || e->rmsf_ok) ? ws.take<float>(rows * (size_t)(d / 64) * 2) : nullptr;
   b.temb_cur = ws.take<float>((size_t)d);
   b.tgrid = ws.take<float>((size_t)nfe);
   b.kstep = ws.take<int>(64);
@@ -853,6 +856,11 @@ static int backbone_part(Ctx& c, int s0, int ns, hipStream_t st) {
   // them; the first layer's attention-norm and the final norm stay launches. lnf(l): layer l's u/v block of the
   // current step's table row (kernels.h LnFoldArgs layout)
   const bool fold_on = c.lnfold && dit && r16 && do_ln && !keep && !chain_on && b.lnp && e->lnf_ok;
+  // UNetT RMSNorm fold (engine.rmsf_ok): the FFN-norm of every layer and the attention-norm of layers 1 .. depth/2 - 1
+  // (whose input FFN2 of the previous layer writes) run inside the GEMMs around them; the consumers read the residual
+  // stream as A with W diag(g). Masked batches too (the producers keep masked rows as they are), but never with the
+  // pad-row skip on a producer (a skipped tile would leave its rows' statistics unwritten)
+  const bool rms_on = c.lnfold && !dit && r16 && b.lnp && e->rmsf_ok;
   const int64_t lnf_lw = 2 * (int64_t)a.ff_dim + 6 * (int64_t)d;
   auto lnf = [&](int l) { return ada_k + e->ada.Npad + (int64_t)l * lnf_lw; };
   auto fold_consumer = [&](GemmArgs& g, const float* u, const float* v) {
@@ -860,6 +868,19 @@ static int backbone_part(Ctx& c, int s0, int ns, hipStream_t st) {
     g.ln_nparts = d / 64;
     g.ln_u = u;
     g.ln_v = v;
+    g.ln_eps = 1e-6f;  // LayerNorm eps (modules.py:316,336)
+  };
+  // RMSNorm form: x / max(|x|, 1e-12) sqrt(d) = x / sqrt(ss / d) (the epsilon only keeps an all-zero row finite)
+  auto rms_consumer = [&](GemmArgs& g) {
+    g.ln_part_in = b.lnp + ro * (size_t)(d / 64) * 2;
+    g.ln_nparts = d / 64;
+    g.ln_rms = 1;
+    g.ln_eps = 1e-30f;
+  };
+  auto rms_producer = [&](GemmArgs& g) {
+    g.ln_part = b.lnp + ro * (size_t)(d / 64) * 2;
+    g.ln_nparts = d / 64;
+    g.ln_rms = 1;
   };
   auto fold_producer = [&](GemmArgs& g, const float* scale) {
     g.hs = aop;
@@ -867,7 +888,7 @@ static int backbone_part(Ctx& c, int s0, int ns, hipStream_t st) {
     g.ln_part = b.lnp + ro * (size_t)(d / 64) * 2;
     g.ln_nparts = d / 64;
   };
-  if (fold_on) e->n_lnfold.fetch_add(1, std::memory_order_relaxed);
+  if (fold_on || rms_on) e->n_lnfold.fetch_add(1, std::memory_order_relaxed);
   for (int l = 0; l < a.depth; ++l) {
     Layer& Ly = e->layers[l];
     const float* ad = ada_k ? ada_k + (size_t)l * 6 * d : nullptr;
@@ -878,7 +899,7 @@ static int backbone_part(Ctx& c, int s0, int ns, hipStream_t st) {
         // the skip connection without a copy
         h_in = res(b.xs[l]);
         h = res(b.xs[l + 1]);
-        KCK(rms_norm_g(bf, h_in, r16, rows, d, Ly.g_attn, aop, st));
+        if (!(rms_on && l > 0)) KCK(rms_norm_g(bf, h_in, r16, rows, d, Ly.g_attn, aop, st));
       } else {
         // x = skip_proj(cat(x, skips.pop())) (unett.py:288-297): ONE GEMM over K = 2d whose A columns
         // [d, 2d) come from the skip buffer; then attention/FFN update the result in place
@@ -898,6 +919,11 @@ static int backbone_part(Ctx& c, int s0, int ns, hipStream_t st) {
     if (!qkv_done) {
       GemmArgs g = qkv_args(Ly);
       if (fold_on && l > 0) fold_consumer(g, lnf(l) + 2 * a.ff_dim, lnf(l) + 2 * a.ff_dim + 3 * d);
+      if (rms_on && l > 0 && l < a.depth / 2) {  // A = the layer input xs[l] itself, W diag(g_attn)
+        g.A = h_in;
+        g.W = Ly.qkv_g.w;
+        rms_consumer(g);
+      }
       ProbeScope ps(e, KC_QKV, st, &c.site, &g.probe);
       KCK(gemm(bf, EPI_QKV, g, st));
     }
@@ -955,15 +981,16 @@ static int backbone_part(Ctx& c, int s0, int ns, hipStream_t st) {
       g.rowkeep = keep;                    // masked_fill of pad rows (modules.py:552-554)
       // row tiles of padding only: no work at all. Only in place (h_in null): a UNetT first-half layer
       // writes x_in + attn into the next buffer, so its pad rows must still be copied there
-      if (keep && !h_in && e->pad_skip) {
+      if (keep && !h_in && e->pad_skip && !rms_on) {
         g.live_len = b.kvlen + s0;
         g.live_seq = c.L;
       }
       if (fold_on) fold_producer(g, ad + 4 * d /*scale_mlp: hs = h (1 + scale_mlp) for FFN1*/);
+      if (rms_on) rms_producer(g);  // the FFN-norm's statistics of h
       ProbeScope ps(e, KC_OUT, st, &c.site, &g.probe);
       KCK(gemm(bf, epi_resid, g, st));
     }
-    if (!fold_on) {
+    if (!fold_on && !rms_on) {
       ProbeScope ps(e, KC_NORM, st, &c.site);
       if (dit) {
         if (do_ln) KCK(ln_modulate(bf, h, r16, rows, d, ad + 3 * d /*shift_mlp*/, ad + 4 * d /*scale_mlp*/, aop, st));
@@ -974,6 +1001,11 @@ static int backbone_part(Ctx& c, int s0, int ns, hipStream_t st) {
     {
       GemmArgs g = gargs(aop, d, Ly.ff1, rows, f, a.ff_dim);
       if (fold_on) fold_consumer(g, lnf(l), lnf(l) + a.ff_dim);
+      if (rms_on) {  // A = h itself, W diag(g_ff)
+        g.A = h;
+        g.W = Ly.ff1_g.w;
+        rms_consumer(g);
+      }
       ProbeScope ps(e, KC_FFN1, st, &c.site, &g.probe);
       KCK(gemm(bf, EPI_GELU_TANH, g, st));
     }
@@ -982,6 +1014,7 @@ static int backbone_part(Ctx& c, int s0, int ns, hipStream_t st) {
       g.gate = ad ? ad + 5 * d : nullptr;  // gate_mlp
       // the next layer's attention-norm: hs = h (1 + scale_msa of layer l + 1) for its QKV
       if (fold_on && l + 1 < a.depth) fold_producer(g, ada_k + (size_t)(l + 1) * 6 * d + d);
+      if (rms_on && l + 1 < a.depth / 2) rms_producer(g);  // the next layer's attention-norm (its input is this h)
       ProbeScope ps(e, KC_FFN2, st, &c.site, &g.probe);
       KCK(gemm(bf, epi_resid, g, st));
     }
@@ -1252,6 +1285,24 @@ int f5h_engine_create_views(const f5h_arch* arch, const f5h_tensor_view* weights
       if (upload(e, wp, &e->lnf_w)) e->lnf_ok = false;
     }
   }
+  // RMSNorm fold support (UNetT, 16-bit): every layer's QKV and FFN1 weights with their norm's gain folded in
+  if (!rc && arch->backbone == F5H_UNETT && e->bf != 0 && arch->dim % 64 == 0 && arch->dim <= 1024) {
+    e->rmsf_ok = true;
+    for (Layer& L : e->layers) {
+      L.qkv_g = L.qkv;
+      L.ff1_g = L.ff1;
+      if (dalloc(e, (size_t)L.qkv.Npad * L.qkv.K * e->esz, &L.qkv_g.w) ||
+          dalloc(e, (size_t)L.ff1.Npad * L.ff1.K * e->esz, &L.ff1_g.w) ||
+          scale_cols(e->bf, L.qkv.w, L.qkv.Npad, L.qkv.K, L.g_attn, L.qkv_g.w, e->mstream) != hipSuccess ||
+          scale_cols(e->bf, L.ff1.w, L.ff1.Npad, L.ff1.K, L.g_ff, L.ff1_g.w, e->mstream) != hipSuccess) {
+        e->rmsf_ok = false;
+        break;
+      }
+    }
+  }
+  // default: on for DiT (C2 -2 %, profiles/r06_ab_fold_c2.txt), off for UNetT (its RMSNorm fold measured within noise
+  // at C5, profiles/r06_ab_rmsfold_c5.txt); F5H_LNFOLD=0/1 or f5h_set_ln_fold overrides
+  e->lnfold = arch->backbone == F5H_DIT ? 1 : 0;
   if (const char* lv = getenv("F5H_LNFOLD")) e->lnfold = (*lv == '0') ? 0 : 1;
   // packing ran on the engine's stream (no device-wide synchronisation)
   if (!rc && hipStreamSynchronize(e->mstream) != hipSuccess) rc = fail(F5H_EHIP, "weight packing");
@@ -1417,7 +1468,7 @@ int f5h_sample(f5h_engine* e, void* stream, const f5h_sample_args* a, void* work
   RC(chain_fault_check(e, c.st));
   ChainTicket ticket;  // (declared after `used`: its event is recorded first, both after every launch of the call)
   c.chain = chain_for_call(e, c, ticket);
-  c.lnfold = e->lnfold && e->lnf_ok && !c.batch_mask && !c.chain;
+  c.lnfold = e->lnfold && !c.chain && ((e->lnf_ok && !c.batch_mask) || e->rmsf_ok);
   double hp[kHostPhases] = {};
   c.hp = hp;
   const double h0 = host_ms();
@@ -1710,7 +1761,7 @@ int f5h_forward(f5h_engine* e, void* stream, const f5h_forward_args* a, void* wo
   RC(chain_fault_check(e, c.st));
   ChainTicket ticket;
   c.chain = chain_for_call(e, c, ticket);
-  c.lnfold = e->lnfold && e->lnf_ok && !c.batch_mask && !c.chain;
+  c.lnfold = e->lnfold && !c.chain && ((e->lnf_ok && !c.batch_mask) || e->rmsf_ok);
   const bool cached = a->text_cache == 2;
   if (a->t_dev) {  // time read on the stream: no host round trip (dit.py:332-333 takes a tensor)
     HIPCK(hipMemcpyAsync(c.b.tgrid, a->t_dev, sizeof(float), hipMemcpyDeviceToDevice, c.st));
@@ -1876,7 +1927,7 @@ int f5h_set_ln_fold(f5h_engine* e, int32_t enable) {
 
 int f5h_ln_fold_stats(f5h_engine* e, int32_t* supported, int64_t* passes) {
   if (!e) return fail(F5H_EINVAL, "null engine");
-  if (supported) *supported = e->lnf_ok ? 1 : 0;
+  if (supported) *supported = (e->lnf_ok || e->rmsf_ok) ? 1 : 0;
   if (passes) *passes = e->n_lnfold.load(std::memory_order_relaxed);
   return 0;
 }

@@ -327,11 +327,47 @@ F5H_DEV float ln_m2_term(float q, float mp, float mean) {
   const float d = sub_nc(mp, mean);
   return __builtin_fmaf(mul_nc(64.f, d), d, q);
 }
-F5H_DEV float ln_rstd(float m2, float inv_np) { return rsqrtf(__builtin_fmaf(m2, mul_nc(inv_np, 1.f / 64.f), 1e-6f)); }
+F5H_DEV float ln_rstd(float m2, float inv_np, float eps) {
+  return rsqrtf(__builtin_fmaf(m2, mul_nc(inv_np, 1.f / 64.f), eps));
+}
 // the 8-lane DPP sum of sum8 over lanes c = 0..7 holding a_c: ((a0 + a1) + (a2 + a3)) + ((a4 + a5) + (a6 + a7)) in
 // every lane (xor 1, xor 2, then the half mirror: lane c adds lane 7 - c, whose pairs are the same sums)
 F5H_DEV float sum8_order(const float (&a)[8]) {
   return add_nc(add_nc(add_nc(a[0], a[1]), add_nc(a[2], a[3])), add_nc(add_nc(a[4], a[5]), add_nc(a[6], a[7])));
+}
+// The once-per-row form of the fold consumer's statistics (LNF 3): thread t < BM of the block fetches row m0 + t's 16
+// strip partials (8 x 16 B; issued whether or not the fold is on — a null descriptor reads zeros with no memory
+// access — so the kernels' counted waits see a constant number of loads), and after the K loop combines them
+// exactly as the per-chunk-row form does (lane c of the row's 8 held partials c and c + 8) into (mean, rstd):
+// every strip holds 64 columns, so mean = the mean of the strip means, M2 = sum of the strips' M2 + 64 sum of
+// (strip mean - mean)^2 (partials past ln_nparts weigh 0).
+F5H_DEV void ln_row_fetch(const GemmArgs& g, int m0, int tid, int BM, u32x4 (&raw)[8]) {
+  const bool on = g.ln_part_in != nullptr;
+  const __amdgpu_buffer_rsrc_t st = rsrc_of(g.ln_part_in, on ? (uint64_t)g.M * g.ln_nparts * 8 : 0);
+  const uint32_t base = tid < BM ? (uint32_t)(min(m0 + tid, g.M - 1) * g.ln_nparts * 8) : 0xFFFFFF00u;
+#pragma unroll
+  for (int e = 0; e < 8; ++e)
+    raw[e] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(st, base + 16 * e, 0, 0));
+}
+F5H_DEV void ln_row_stats(const GemmArgs& g, const u32x4 (&raw)[8], float* out) {
+  const int np = g.ln_nparts;
+  const float inv_np = 1.f / (float)np;
+  auto mp = [&](int p) { return __uint_as_float(raw[p >> 1][(p & 1) * 2]); };
+  auto qp = [&](int p) { return __uint_as_float(raw[p >> 1][(p & 1) * 2 + 1]); };
+  float a[8], e[8];
+#pragma unroll
+  for (int c = 0; c < 8; ++c) {
+    const float w0 = c < np ? 1.f : 0.f, w1 = c + 8 < np ? 1.f : 0.f;
+    a[c] = add_nc(w0 * mp(c), w1 * mp(c + 8));
+  }
+  const float mean = mul_nc(sum8_order(a), inv_np);
+#pragma unroll
+  for (int c = 0; c < 8; ++c) {
+    const float w0 = c < np ? 1.f : 0.f, w1 = c + 8 < np ? 1.f : 0.f;
+    e[c] = add_nc(w0 * ln_m2_term(qp(c), mp(c), mean), w1 * ln_m2_term(qp(c + 8), mp(c + 8), mean));
+  }
+  out[0] = mean;
+  out[1] = ln_rstd(sum8_order(e), inv_np, g.ln_eps);
 }
 
 // Fast epilogue of one wave's sub-tile (whole-column tiles of the hot epilogues), per 16-row strip:
@@ -363,7 +399,7 @@ F5H_DEV void epilogue_fast_t(const GemmArgs& g, const f32x4 (&acc)[MT][NT], floa
   constexpr int TPC = 16 * CH / 64;   // chunks per lane per strip
   static_assert(64 % CH == 0 && (16 * CH) % 64 == 0, "whole chunks per lane");
   static_assert(LNF == 0 || (WN == 64 && is16<TC>()), "the LayerNorm fold: 64-column wave strips, 16-bit operands");
-  static_assert(LNF != 1 || EPI == EPI_RESID16, "fold producer: the 16-bit residual epilogue");
+  static_assert((LNF != 1 && LNF != 4) || EPI == EPI_RESID16, "fold producer: the 16-bit residual epilogue");
   static_assert(!LNCONS || EPI == EPI_GELU_TANH || EPI == EPI_QKV, "fold consumer: FFN1 or QKV");
   const int fr = lane & 15, q = lane >> 4;
   const int cc = lane % CH;
@@ -376,16 +412,18 @@ F5H_DEV void epilogue_fast_t(const GemmArgs& g, const f32x4 (&acc)[MT][NT], floa
   __amdgpu_buffer_rsrc_t ln_dst = rsrc_of(nullptr, 0), ln_st = rsrc_of(nullptr, 0);
   int ln_p = 0;
   const int ln_np = g.ln_nparts;
-  if constexpr (LNF == 1) {
-    lnA = load8(g.hs_scale + col);
+  if constexpr (LNF == 1 || LNF == 4) {
+    if constexpr (LNF == 1) {
+      lnA = load8(g.hs_scale + col);
 #pragma unroll
-    for (int e = 0; e < 8; ++e) lnA.v[e] = 1.f + lnA.v[e];
-    ln_dst = rsrc_of(g.hs, (uint64_t)g.M * g.ldc * sizeof(TC));
+      for (int e = 0; e < 8; ++e) lnA.v[e] = 1.f + lnA.v[e];
+      ln_dst = rsrc_of(g.hs, (uint64_t)g.M * g.ldc * sizeof(TC));
+    }
     ln_st = rsrc_of(g.ln_part, (uint64_t)g.M * ln_np * 8);
     ln_p = __builtin_amdgcn_readfirstlane(cbase >> 6);
   } else if constexpr (LNCONS) {
-    lnA = load8(g.ln_u + col);
-    lnB = load8(g.ln_v + col);
+    if (g.ln_u) lnA = load8(g.ln_u + col);  // (RMSNorm form: u = v = 0, the gain is in W)
+    if (g.ln_v) lnB = load8(g.ln_v + col);
     if constexpr (BIAS) {  // the bias joins v: one fused multiply-add pair per element below
 #pragma unroll
       for (int e = 0; e < 8; ++e) lnB.v[e] += bias8.v[e];
@@ -527,7 +565,7 @@ F5H_DEV void epilogue_fast_t(const GemmArgs& g, const f32x4 (&acc)[MT][NT], floa
         const float m0 = __uint_as_float(ri.s0.x), m1 = __uint_as_float(ri.s1.x);
         m = mul_nc(sum8(add_nc(ln_w0 * m0, ln_w1 * m1)), ln_inv_np);
         const float e0 = ln_m2_term(__uint_as_float(ri.s0.y), m0, m), e1 = ln_m2_term(__uint_as_float(ri.s1.y), m1, m);
-        rstd = ln_rstd(sum8(add_nc(ln_w0 * e0, ln_w1 * e1)), ln_inv_np);
+        rstd = ln_rstd(sum8(add_nc(ln_w0 * e0, ln_w1 * e1)), ln_inv_np, g.ln_eps);
         }
         // x = rstd (x - m u) + (v + bias), as packed fp32 FMAs on column pairs
 #pragma unroll
@@ -574,23 +612,26 @@ F5H_DEV void epilogue_fast_t(const GemmArgs& g, const f32x4 (&acc)[MT][NT], floa
 #pragma unroll
         for (int e = 0; e < 8; ++e) o.v[e] = resid_add(c.v[e], gate8.v[e], x.v[e], keep);
         store8_rs<ResT<TC, EPI>, AUX>(dst, (uint32_t)((int64_t)row * g.ldc + col), o);
-        if constexpr (LNF == 1) {
+        if constexpr (LNF == 1 || LNF == 4) {
           // the stored (rounded) h values: hs = h (1 + scale) for the consumer, and this 64-column strip's
-          // (mean, M2) of h (two passes over the row's 8 lanes)
+          // (mean, M2) of h (two passes over the row's 8 lanes). RMSNorm form (LNF 4): no hs, and the strip's
+          // "mean" is 0, so its M2 is the sum of squares the consumer needs
           V8 hr, hv;
           f32x2 s2 = {0.f, 0.f};
 #pragma unroll
           for (int e = 0; e < 8; e += 2) {
             const f32x2 h2 = {to_f32(from_f32<TC>(o.v[e])), to_f32(from_f32<TC>(o.v[e + 1]))};
-            const f32x2 v2 = h2 * f32x2{lnA.v[e], lnA.v[e + 1]};
             hr.v[e] = h2.x;
             hr.v[e + 1] = h2.y;
-            hv.v[e] = v2.x;
-            hv.v[e + 1] = v2.y;
-            s2 += h2;
+            if constexpr (LNF == 1) {
+              const f32x2 v2 = h2 * f32x2{lnA.v[e], lnA.v[e + 1]};
+              hv.v[e] = v2.x;
+              hv.v[e + 1] = v2.y;
+              s2 += h2;
+            }
           }
-          store8_rs<TC, AUX>(ln_dst, (uint32_t)((int64_t)row * g.ldc + col), hv);
-          const float mean = sum8(s2.x + s2.y) * (1.f / 64.f);
+          if constexpr (LNF == 1) store8_rs<TC, AUX>(ln_dst, (uint32_t)((int64_t)row * g.ldc + col), hv);
+          const float mean = LNF == 4 ? 0.f : sum8(s2.x + s2.y) * (1.f / 64.f);
           f32x2 q2 = {0.f, 0.f};
 #pragma unroll
           for (int e = 0; e < 8; e += 2) {
@@ -648,7 +689,14 @@ F5H_DEV void epilogue_fast(const GemmArgs& g, const f32x4 (&acc)[MT][NT], float*
   // LayerNorm fold forms (GemmArgs hs / ln_part_in: 16-bit, 64-column wave strips; bias always present there)
   if constexpr (WN == 64 && is16<TC>() && AUX == 0) {
     if constexpr (EPI == EPI_RESID16) {
-      if (g.hs) {
+      if (g.ln_part && g.ln_rms) {
+        if (g.bias)
+          epilogue_fast_t<TC, EPI, MT, NT, WN, EPAD, PREF, true, PM, PT, AUX, PD, 4>(g, acc, Cs, rbase, cbase, lane, pre);
+        else
+          epilogue_fast_t<TC, EPI, MT, NT, WN, EPAD, PREF, false, PM, PT, AUX, PD, 4>(g, acc, Cs, rbase, cbase, lane, pre);
+        return;
+      }
+      if (g.ln_part) {
         if (g.bias)
           epilogue_fast_t<TC, EPI, MT, NT, WN, EPAD, PREF, true, PM, PT, AUX, PD, 1>(g, acc, Cs, rbase, cbase, lane, pre);
         else
@@ -1058,14 +1106,7 @@ F5H_DEV void gemm_body(const GemmArgs& g, const int b, const int nwg, uint4* lds
   constexpr bool LNC = (EPI == EPI_QKV || EPI == EPI_GELU_TANH) && is16<TC>() && WN == 64 && FAST && NT % 2 == 0 &&
                        !CHAIN && !PUB && BM <= C::THREADS;
   u32x4 lnraw[LNC ? 8 : 1];
-  if constexpr (LNC) {
-    const bool on = g.ln_part_in != nullptr;
-    const __amdgpu_buffer_rsrc_t st = rsrc_of(g.ln_part_in, on ? (uint64_t)g.M * g.ln_nparts * 8 : 0);
-    const uint32_t base = tid < BM ? (uint32_t)(min(m0 + tid, g.M - 1) * g.ln_nparts * 8) : 0xFFFFFF00u;
-#pragma unroll
-    for (int e = 0; e < 8; ++e)
-      lnraw[e] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(st, base + 16 * e, 0, 0));
-  }
+  if constexpr (LNC) ln_row_fetch(g, m0, tid, BM, lnraw);
   constexpr int NPRE = PREF ? MT * TPS : (LNC ? 8 : 0);  // loads issued behind the first stages
   for (int kt = 0; kt < nk; ++kt) {
     // stage kt has landed for THIS wave once at most the younger in-flight stages remain;
@@ -1148,29 +1189,7 @@ F5H_DEV void gemm_body(const GemmArgs& g, const int b, const int nwg, uint4* lds
   if constexpr (LNC) {
     static_assert(C::bytes >= (NW * 16 * C::EPAD + 2 * BM) * 4, "LDS for the fold's row statistics");
     if (g.ln_part_in) {  // uniform
-      if (tid < BM) {
-        // every strip holds 64 columns: mean = the mean of the strip means, M2 = sum of the strips' M2 + 64 sum of
-        // (strip mean - mean)^2 (partials past ln_nparts weigh 0)
-        // the epilogue's per-chunk-row form, bit for bit: lane c of the row's 8 held partials c and c + 8
-        const int np = g.ln_nparts;
-        const float inv_np = 1.f / (float)np;
-        auto mp = [&](int p) { return __uint_as_float(lnraw[p >> 1][(p & 1) * 2]); };
-        auto qp = [&](int p) { return __uint_as_float(lnraw[p >> 1][(p & 1) * 2 + 1]); };
-        float a[8], e[8];
-#pragma unroll
-        for (int c = 0; c < 8; ++c) {
-          const float w0 = c < np ? 1.f : 0.f, w1 = c + 8 < np ? 1.f : 0.f;
-          a[c] = add_nc(w0 * mp(c), w1 * mp(c + 8));
-        }
-        const float mean = mul_nc(sum8_order(a), inv_np);
-#pragma unroll
-        for (int c = 0; c < 8; ++c) {
-          const float w0 = c < np ? 1.f : 0.f, w1 = c + 8 < np ? 1.f : 0.f;
-          e[c] = add_nc(w0 * ln_m2_term(qp(c), mp(c), mean), w1 * ln_m2_term(qp(c + 8), mp(c + 8), mean));
-        }
-        ln_rows[2 * tid] = mean;
-        ln_rows[2 * tid + 1] = ln_rstd(sum8_order(e), inv_np);
-      }
+      if (tid < BM) ln_row_stats(g, lnraw, ln_rows + 2 * tid);
       __syncthreads();
     }
   }
@@ -1373,6 +1392,13 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(GemmArgs g) {
   };
 
   const int nph = g.K / (32 * KS);
+  // LayerNorm / RMSNorm fold consumer: the block's rows' strip partials (ln_row_fetch), issued AHEAD of the prologue
+  // DMA, so every counted wait below stays exact (they are the oldest loads: the first wait retires them with phase
+  // 0). Behind the DMA they made the first in-loop wait retire phase 2 early: +1 us of ramp per C5 FFN1 tile.
+  constexpr bool LNC = (EPI == EPI_QKV || EPI == EPI_GELU_TANH) && is16<TC>() && WN == 64 && FAST && NT % 2 == 0 &&
+                       BM <= 512;
+  u32x4 lnraw[LNC ? 8 : 1];
+  if constexpr (LNC) ln_row_fetch(g, m0, tid, BM, lnraw);
   for (int p = 0; p < D && p < nph; ++p) dma_phase(p);
   wait_dma(0, min(D, nph) - 1);
   __builtin_amdgcn_s_barrier();
@@ -1408,8 +1434,17 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(GemmArgs g) {
     __builtin_amdgcn_sched_barrier(0);
   }
   if (grp == 0) __builtin_amdgcn_s_barrier();  // matches group 1's extra barrier
+  __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0) (hand-written waits above are invisible to hipcc)
   __syncthreads();
   probe_mark(g.probe, probe_t, 2);
+  float* const ln_rows = reinterpret_cast<float*>(lds) + 8 * 16 * C::EPAD;  // past the 8 wave strips
+  if constexpr (LNC) {
+    static_assert(C::bytes >= (8 * 16 * C::EPAD + 2 * BM) * 4, "LDS for the fold's row statistics");
+    if (g.ln_part_in) {  // uniform
+      if (tid < BM) ln_row_stats(g, lnraw, ln_rows + 2 * tid);
+      __syncthreads();
+    }
+  }
 
   // ---- epilogue: as gemm_kernel, per wave and 16-row strip through LDS
   float* Cs = reinterpret_cast<float*>(lds) + wid * 16 * C::EPAD;
@@ -1419,7 +1454,8 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(GemmArgs g) {
     // whole-column tiles: the strip-pipelined epilogue (the generic one below waits out every strip's
     // residual / RoPE loads before its stores: 13-15 us per 256x256 tile at C3, profiles/r03_timeline_c3.txt)
     const V8 none[1][1] = {};
-    epilogue_fast<TC, EPI, MT, NT, WN, C::EPAD, false>(g, acc, Cs, rbase, cbase, lane, none);
+    epilogue_fast<TC, EPI, MT, NT, WN, C::EPAD, false>(g, acc, Cs, rbase, cbase, lane, none,
+                                                       LNC ? ln_rows + 2 * (grp * (BM / 2) + wm * WM) : nullptr);
   } else {
 #pragma unroll
   for (int i = 0; i < MT; ++i) {
@@ -1981,13 +2017,20 @@ static hipError_t launch_t(const GemmArgs& a, hipStream_t st) {
   // 256x256 configuration without it (12: 32-column quadrant strips, 13: register-only epilogue) runs as cfg 11, the
   // same tile (every configuration gives the same bits); anything else is refused rather than ignored (the results
   // would be those of an unnormalised operand)
-  if ((a.hs || a.ln_part_in) && (cfg == 12 || cfg == 13)) cfg = 11;
-  if (a.hs || a.ln_part_in) {
-    const bool prod = a.hs && EPI == EPI_RESID16 && a.hs_scale && a.ln_part;
-    const bool cons = a.ln_part_in && (EPI == EPI_GELU_TANH || EPI == EPI_QKV) && a.ln_u && a.ln_v;
+  if ((a.ln_part || a.ln_part_in) && (cfg == 12 || cfg == 13)) cfg = 11;
+  // a 256x256 tile needs whole 256-column tiles for the strip epilogue: narrower outputs take the 128x128 tile
+  if ((a.ln_part || a.ln_part_in) && cfg == 11 && !fast_epi_ok<EPI>(a, 256)) cfg = 1;
+  if (a.hs || a.ln_part || a.ln_part_in) {
+    // LayerNorm form: producer hs + hs_scale, consumer u + v; RMSNorm form (ln_rms): neither. Row masks only with the
+    // RMSNorm form (the DiT fold runs on unmasked rows; UNetT batches keep their masks), never the pad-row skip (a
+    // skipped tile would leave its rows' statistics unwritten)
+    const bool prod = a.ln_part && EPI == EPI_RESID16 && (a.ln_rms ? !a.hs && !a.hs_scale : a.hs && a.hs_scale);
+    const bool cons = a.ln_part_in && (EPI == EPI_GELU_TANH || EPI == EPI_QKV) &&
+                      (a.ln_rms ? !a.ln_u && !a.ln_v : a.ln_u && a.ln_v);
     const int bn = cfg == 11 ? 256 : 128;
-    if (!is16<TC>() || (a.hs && a.ln_part_in) || !(prod || cons) || a.ln_nparts <= 0 || a.ln_nparts > 16 ||
-        (cfg != 0 && cfg != 1 && cfg != 5 && cfg != 11) || !fast_epi_ok<EPI>(a, bn) || a.rowkeep || a.live_len)
+    if (!is16<TC>() || (a.ln_part && a.ln_part_in) || !(prod || cons) || a.ln_nparts <= 0 || a.ln_nparts > 16 ||
+        (cfg != 0 && cfg != 1 && cfg != 5 && cfg != 11) || !fast_epi_ok<EPI>(a, bn) || (a.rowkeep && !a.ln_rms) ||
+        a.live_len)
       return hipErrorInvalidValue;
   }
   switch (cfg) {

@@ -76,6 +76,11 @@ struct GemmArgs {
   //   ln_u[n] = sum_k (1 + sc_k) W[n,k] and ln_v[n] = sum_k sh_k W[n,k] (lnfold_uv, per ODE step).
   void* hs; const float* hs_scale; float* ln_part;
   const float* ln_part_in; int ln_nparts; const float* ln_u; const float* ln_v;
+  // RMSNorm form (UNetT, x_transformers RMSNorm: x / max(|x|, 1e-12) sqrt(d) g): ln_rms = 1. The producer writes
+  // (0, sum of squares) per strip and no hs (hs, hs_scale null); the consumer reads the residual stream itself as A,
+  // its W already carries the gain (W' = W diag(g), built once), ln_u / ln_v are null (0) and rstd = 1 / sqrt(ss / d +
+  // ln_eps). ln_eps: the consumer's variance epsilon (LayerNorm: 1e-6, modules.py:316,336).
+  int ln_rms; float ln_eps;
 };
 
 // Does the row tile [m0, m0 + BM) of an M-row GEMM hold a live row? Sequence s (rows [s*live_seq, (s+1)*live_seq))
@@ -142,6 +147,8 @@ hipError_t ln_modulate(int compute, const void* h, int h16, int M, int d, const 
 // x_transformers RMSNorm: x / max(||x||, 1e-12) * sqrt(d) * g -> operand dtype
 // h: fp32, or the operand dtype when h16 (16-bit residual stream)
 hipError_t rms_norm_g(int compute, const void* h, int h16, int M, int d, const float* g, void* out, hipStream_t st);
+// out[n][k] = round(W[n][k] g[k]) for rows x K 16-bit W (the RMSNorm fold's W' = W diag(g), built once per engine)
+hipError_t scale_cols(int compute, const void* W, int64_t rows, int K, const float* g, void* out, hipStream_t st);
 hipError_t rope_table(int L, float2* out, hipStream_t st);
 // text tokens -> embeddings (dit.py:86-120 / unett.py:53-64), both branches
 struct TextEmbArgs {

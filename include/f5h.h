@@ -232,8 +232,12 @@ int f5h_set_chain(f5h_engine* eng, int32_t enable);
  * (mean, M2) partials of h, the consumer normalises its accumulators, rstd (acc - mean u) + v with per-step vectors
  * u = (1 + scale) W^T, v = shift W^T computed once per call. Not bitwise the separate launches (the statistics and
  * the rounding point move): within the reduced-precision envelopes (tests/test_gpu_envelope.py). 1 (default) or 0
- * (env F5H_LNFOLD=0 at creation: 0). f5h_ln_fold_stats: *supported = 1 when the engine can fold (DiT, 16-bit,
- * dim and ff_dim multiples of 64, dim <= 1024), *passes = backbone passes enqueued with the fold. */
+ * (env F5H_LNFOLD=0 at creation: 0). The same switch covers the UNetT RMSNorm fold (default 0 on UNetT engines,
+ * F5H_LNFOLD=1: on; unett.py:300-301, x_transformers
+ * RMSNorm): every FFN-norm and the attention-norms of the first half's layers 1.., on masked batches too; the
+ * producers write per-row sums of squares, the consumers read the residual stream with W diag(g) built once per
+ * engine. f5h_ln_fold_stats: *supported = 1 when the engine can fold (16-bit DiT with dim and ff_dim multiples of
+ * 64, or 16-bit UNetT with dim a multiple of 64; dim <= 1024), *passes = backbone passes enqueued with a fold. */
 int f5h_set_ln_fold(f5h_engine* eng, int32_t enable);
 int f5h_ln_fold_stats(f5h_engine* eng, int32_t* supported, int64_t* passes);
 /* Failure of the chain (never expected): a chain wait that gives up (a bounded spin of ~0.3 s) sets the

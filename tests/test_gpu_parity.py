@@ -171,6 +171,51 @@ def test_ln_fold_bitwise_identical_across_tile_configs(compute, preset, depth):
     assert rel < (1e-2 if compute == "bf16" else 2e-3), rel
 
 
+@pytest.mark.parametrize("compute", ["bf16", "fp16"])
+@pytest.mark.parametrize("preset,depth,spec", [
+    ("E2TTS_Base", 4, dict(B=2, ref_frames=[100, 60], total_frames=[300, 220], n_text=[50, 40])),
+    ("UNetT_tiny", 4, dict(B=1, ref_frames=[70], total_frames=[190], n_text=[30], vocab=64))])
+def test_rms_fold_unett(compute, preset, depth, spec):
+    """The UNetT RMSNorm fold (x_transformers RMSNorm, unett.py:300-301: the FFN-norms and the first half's
+    attention-norms inside the GEMMs around them; the consumers read the residual stream with W diag(g)): on a masked
+    batch with ragged lengths and on one utterance, bitwise identical under every tile configuration, and against
+    the RMSNorm launches only the rounding moves (W diag(g) rounded once per weight instead of the normalised
+    activations per element; rel-L2 well under the 16-bit output rounding's order)."""
+    _need_gpu()
+    from f5_tts_amd import configs
+
+    over = {"depth": depth} if preset == "E2TTS_Base" else {"text_num_embeds": 64}
+    arch = configs.get_arch(preset, **over)
+    m = _model(arch, compute)
+    eng = m.transformer.get_engine(compute, m.device)
+    inp = synthetic.make_case(**spec)
+    dur = torch.tensor(spec["total_frames"])
+    y0 = synthetic.reference_noise(dur, 9)
+    kw = dict(cond=inp["cond"].to(DEV), text=inp["text"].to(DEV), duration=dur.to(DEV), lens=inp["lens"].to(DEV),
+              y0=y0.to(DEV), steps=3, cfg_strength=2.0, sway_sampling_coef=-1.0, keep_trajectory=False)
+    outs = []
+    try:
+        eng.set_ln_fold(True)
+        sup, p0 = eng.ln_fold_stats()
+        assert sup, "the RMSNorm fold should be supported for this architecture"
+        for cfg in GEMM_CONFIGS:
+            gemm_force_config(cfg)
+            outs.append(m.sample(**kw)[0].clone())
+        _, p1 = eng.ln_fold_stats()
+        assert p1 > p0, "no backbone pass ran with the fold"
+        gemm_force_config(-1)
+        eng.set_ln_fold(False)
+        plain = m.sample(**kw)[0]
+    finally:
+        gemm_force_config(-1)
+        eng.set_ln_fold(os.environ.get("F5H_LNFOLD") == "1")  # UNetT engines: off unless asked for
+    assert torch.isfinite(outs[0]).all()
+    for cfg, o in zip(GEMM_CONFIGS, outs):
+        assert torch.equal(o, outs[0]), cfg
+    rel = float((outs[0].float() - plain.float()).norm() / plain.float().norm())
+    assert rel < (1e-2 if compute == "bf16" else 2e-3), rel
+
+
 @pytest.mark.parametrize("compute,tol", [("fp32", 1e-5), ("bf16", 2e-2), ("fp16", 4e-3)])
 @pytest.mark.parametrize("S,H,N,masked", [(2, 16, 1876, False), (3, 2, 150, True), (1, 1, 65, False),
                                           (2, 4, 577, True)])
