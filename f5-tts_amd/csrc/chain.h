@@ -6,8 +6,9 @@
 //     row group its tile covers;
 //   consumer workgroup: ONE wave polls each needed counter (relaxed agent loads + s_sleep, bounded) -> ONE
 //     agent-scope acquire (drops this CU's L1) -> s_waitcnt vmcnt(0) -> __syncthreads() -> plain loads.
-// Counters are zeroed by one memset node per step (Guideline 16, 'Re-initialise every call'): each layer's launch
-// has its own [5][groups] block of them.
+// Counters are zeroed by a kernel (zero_words) at the start of every backbone pass (Guideline 16, 'Re-initialise
+// every call'; a captured memset node was not re-applied on later replays of the step graph, round 6): each layer's
+// launch has its own [5][groups] block of them.
 // Progress: a phase's workgroups have higher ids than every producer they wait for, and the dispatcher hands
 // out ids in order on each XCD, so every producer is resident or finished before any consumer can wait on it
 // (a waiting block never keeps a producer from being dispatched). The bounded spin only guards against a bug:
